@@ -1,0 +1,251 @@
+"""Device-resident batch codec over PyTorch-ROCm buffers (calls the C ABI).
+
+This is the engine under the reference-shaped aggregators: one call encodes a
+round's batch of client deltas (``fc_quantize_encode``), one call decodes and
+sums them (``fc_decode_accumulate``).  All buffers stay in HBM; the only host
+syncs are the overflow check and the small per-client measurement vectors.
+"""
+import numpy as np
+import torch
+
+from federated_amd import _lib
+
+_ALIGN = 64
+
+
+def _round_up(x, a):
+  return (int(x) + a - 1) // a * a
+
+
+def num_tiles(P):
+  return (int(P) + _lib.TILE_ELEMS - 1) // _lib.TILE_ELEMS
+
+
+def default_capacity(P):
+  """Bytes reserved per client code: 4 bits/element + slack; grown on overflow."""
+  return _round_up(P // 2 + 256, _ALIGN)
+
+
+def worst_case_capacity(P):
+  """<= 65 bits per element (+ trailing run code), in whole 16-byte blocks."""
+  return _round_up((65 * int(P) + 64) // 8 + 64, _ALIGN)
+
+
+class EncodedBatch:
+  """Run-length-gamma codes of a batch of clients, resident in HBM."""
+
+  def __init__(self, P, nclients, caps, device):
+    self.P = int(P)
+    self.nclients = int(nclients)
+    self.T = num_tiles(P)
+    self.device = device
+    caps = [int(_round_up(c, _ALIGN)) for c in caps]
+    offs = np.zeros(self.nclients, np.int64)
+    offs[1:] = np.cumsum(caps)[:-1]
+    self.caps_host = np.asarray(caps, np.int64)
+    self.offs_host = offs
+    self.stream = torch.empty(int(sum(caps)) + _ALIGN, dtype=torch.uint8, device=device)
+    self.stream_off = torch.from_numpy(offs).to(device)
+    self.stream_cap = torch.from_numpy(self.caps_host).to(device)
+    self.idx = torch.empty(self.nclients * (self.T + 1), dtype=torch.int64, device=device)
+    self.total_bits = torch.empty(self.nclients, dtype=torch.int64, device=device)
+    self.overflow = torch.zeros(self.nclients, dtype=torch.int32, device=device)
+    self.dist_part = torch.empty(self.nclients * self.T, dtype=torch.float32, device=device)
+    self.nnz_part = torch.empty(self.nclients * self.T, dtype=torch.int32, device=device)
+
+  def bits(self):
+    return self.total_bits.cpu().numpy()
+
+  def nbytes(self):
+    return (self.bits() + 7) // 8
+
+  def client_code(self, c):
+    """Canonical TFC byte string of client c (D2H copy)."""
+    nb = int((int(self.total_bits[c].item()) + 7) // 8)
+    off = int(self.offs_host[c])
+    return bytes(self.stream[off:off + nb].cpu().numpy().tobytes())
+
+
+class Workspace:
+  """Grow-only device workspace for the encoder's look-back status array."""
+
+  def __init__(self):
+    self.buf = None
+
+  def get(self, nclients, P, device):
+    need = int(_lib.load().fc_encode_workspace_bytes(int(nclients), int(P)))
+    if self.buf is None or self.buf.numel() < need or self.buf.device != device:
+      self.buf = torch.empty(_round_up(need, 256), dtype=torch.uint8, device=device)
+    return self.buf
+
+
+_WS = Workspace()
+
+
+def _ptr_array(tensors, device):
+  return torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64, device=device)
+
+
+def _rows(xs, dtype):
+  """List of contiguous 1-D device tensors from a [C, P] tensor or a list."""
+  if isinstance(xs, torch.Tensor):
+    assert xs.dim() == 2
+    xs = [xs[i] for i in range(xs.shape[0])]
+  rows = []
+  for x in xs:
+    x = torch.as_tensor(x)
+    if not x.is_cuda:
+      x = x.cuda()
+    x = x.reshape(-1).to(dtype).contiguous()
+    rows.append(x)
+  return rows
+
+
+def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, ptrs=None,
+                    out=None, P=None):
+  """fc_quantize_encode over a batch.  ``xs``: [C, P] tensor or list of tensors.
+
+  ``seeds``: int64 tensor [C, 2] (device or host).  ``norms``: optional device
+  float32 [C] (client step = norms[c] * step).  Returns an EncodedBatch.
+  ``ptrs``/``P``/``out`` let hot loops reuse a pointer array and buffers.
+  """
+  _lib.require_gpu()
+  if ptrs is None:
+    rows = _rows(xs, torch.float32)
+    P = rows[0].numel()
+    assert all(r.numel() == P for r in rows)
+    device = rows[0].device
+    ptrs = _ptr_array(rows, device)
+  device = ptrs.device
+  C = ptrs.numel()
+  seeds = torch.as_tensor(seeds, dtype=torch.int64).reshape(C, 2).to(device)
+  if out is None:
+    out = EncodedBatch(P, C, caps if caps is not None else [default_capacity(P)] * C, device)
+  ws = _WS.get(C, P, device)
+  _lib.call("fc_quantize_encode", _lib.ptr(ptrs), C, P, float(step), _lib.ptr(norms),
+            _lib.ptr(seeds), int(mode), _lib.ptr(out.stream), _lib.ptr(out.stream_off),
+            _lib.ptr(out.stream_cap), _lib.ptr(out.idx), _lib.ptr(out.total_bits),
+            _lib.ptr(out.dist_part), _lib.ptr(out.nnz_part), _lib.ptr(out.overflow),
+            _lib.ptr(ws), ws.numel(), _lib.stream_handle(stream))
+  return out
+
+
+def check_overflow(batch):
+  """Host check; returns indices of clients whose capacity was too small."""
+  return np.nonzero(batch.overflow.cpu().numpy())[0]
+
+
+def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None):
+  """quantize_encode, re-encoding with worst-case capacity if any client overflowed."""
+  rows = _rows(xs, torch.float32)
+  P = rows[0].numel()
+  batch = quantize_encode(rows, step, seeds, mode, norms=norms, caps=caps)
+  if len(check_overflow(batch)):
+    batch = quantize_encode(rows, step, seeds, mode, norms=norms,
+                            caps=[worst_case_capacity(P)] * len(rows))
+    assert not len(check_overflow(batch))
+  return batch
+
+
+def rlgamma_encode(qs, caps=None):
+  """tfc.run_length_gamma_encode over a batch of int32 tensors (device)."""
+  _lib.require_gpu()
+  rows = _rows(qs, torch.int32)
+  P = rows[0].numel()
+  device = rows[0].device
+  C = len(rows)
+  ptrs = _ptr_array(rows, device)
+  out = EncodedBatch(P, C, caps if caps is not None else [worst_case_capacity(P)] * C, device)
+  ws = _WS.get(C, P, device)
+  _lib.call("fc_rlgamma_encode", _lib.ptr(ptrs), C, P, _lib.ptr(out.stream),
+            _lib.ptr(out.stream_off), _lib.ptr(out.stream_cap), _lib.ptr(out.idx),
+            _lib.ptr(out.total_bits), _lib.ptr(out.overflow), _lib.ptr(ws), ws.numel(),
+            _lib.stream_handle())
+  return out
+
+
+def decode_accumulate(batch, sum_in=None, want_sum=True, out=None, step=1.0, noise_sum=None,
+                      stream=None, err=None, sum_out=None):
+  """Decode every client's code and sum over clients (int32, wrapping).
+
+  Returns (sum_out or None, out or None, err tensor).
+  """
+  _lib.require_gpu()
+  device = batch.device
+  if want_sum and sum_out is None:
+    sum_out = torch.empty(batch.P, dtype=torch.int32, device=device)
+  if err is None:
+    err = torch.zeros(1, dtype=torch.int32, device=device)
+  _lib.call("fc_decode_accumulate", _lib.ptr(batch.stream), _lib.ptr(batch.stream_off),
+            _lib.ptr(batch.stream_cap), _lib.ptr(batch.idx), batch.nclients, batch.P,
+            _lib.ptr(sum_in), _lib.ptr(sum_out if want_sum else None), _lib.ptr(out),
+            float(step), _lib.ptr(noise_sum), _lib.ptr(err), _lib.stream_handle(stream))
+  return (sum_out if want_sum else None), out, err
+
+
+def finalize(batch, stream=None):
+  """Per-client float64 sum of squared error and int64 nonzero count (device)."""
+  dist = torch.empty(batch.nclients, dtype=torch.float64, device=batch.device)
+  nnz = torch.empty(batch.nclients, dtype=torch.int64, device=batch.device)
+  _lib.call("fc_finalize", _lib.ptr(batch.dist_part), _lib.ptr(batch.nnz_part), batch.nclients,
+            batch.P, _lib.ptr(dist), _lib.ptr(nnz), _lib.stream_handle(stream))
+  return dist, nnz
+
+
+def quantize(x, step, seed, mode, want_noise=False):
+  """Elementwise quantiser of one tensor: returns (q int32, noise float32 or None)."""
+  _lib.require_gpu()
+  x = _rows([x], torch.float32)[0]
+  q = torch.empty(x.numel(), dtype=torch.int32, device=x.device)
+  noise = torch.empty(x.numel(), dtype=torch.float32, device=x.device) if want_noise else None
+  _lib.call("fc_quantize", _lib.ptr(x), x.numel(), float(step), int(seed[0]), int(seed[1]),
+            int(mode), _lib.ptr(q), _lib.ptr(noise), _lib.stream_handle())
+  return q, noise
+
+
+def dequantize(s, step, noise_sum=None):
+  _lib.require_gpu()
+  out = torch.empty(s.numel(), dtype=torch.float32, device=s.device)
+  _lib.call("fc_dequantize", _lib.ptr(s), s.numel(), float(step), _lib.ptr(noise_sum),
+            _lib.ptr(out), _lib.stream_handle())
+  return out
+
+
+def noise_sum(seeds, P, device):
+  seeds = torch.as_tensor(seeds, dtype=torch.int64).reshape(-1, 2).to(device)
+  out = torch.empty(int(P), dtype=torch.float32, device=device)
+  _lib.call("fc_noise_sum", _lib.ptr(seeds), seeds.shape[0], int(P), _lib.ptr(out),
+            _lib.stream_handle())
+  return out
+
+
+def client_norms(xs, kind):
+  rows = _rows(xs, torch.float32)
+  P = rows[0].numel()
+  ptrs = _ptr_array(rows, rows[0].device)
+  norms = torch.empty(len(rows), dtype=torch.float32, device=rows[0].device)
+  _lib.call("fc_client_norms", _lib.ptr(ptrs), len(rows), P, int(kind), _lib.ptr(norms),
+            _lib.stream_handle())
+  return norms
+
+
+def onebit_encode(xs, threshold=0.0):
+  rows = _rows(xs, torch.float32)
+  P = rows[0].numel()
+  device = rows[0].device
+  C = len(rows)
+  ptrs = _ptr_array(rows, device)
+  nw = (P + 31) // 32
+  masks = torch.empty(C * nw, dtype=torch.int32, device=device)
+  means = torch.empty(2 * C, dtype=torch.float32, device=device)
+  dist = torch.empty(C, dtype=torch.float64, device=device)
+  _lib.call("fc_onebit_encode", _lib.ptr(ptrs), C, P, float(threshold), _lib.ptr(masks),
+            _lib.ptr(means), _lib.ptr(dist), _lib.stream_handle())
+  return masks, means, dist
+
+
+def onebit_decode_sum(masks, means, nclients, P):
+  out = torch.empty(int(P), dtype=torch.float32, device=masks.device)
+  _lib.call("fc_onebit_decode_sum", _lib.ptr(masks), _lib.ptr(means), int(nclients), int(P),
+            _lib.ptr(out), _lib.stream_handle())
+  return out

@@ -1,0 +1,146 @@
+/* fedcodec: MI355X-native client-update codec for compressed_communication/.
+ *
+ * C ABI of libfedcodec.so (federated_amd/csrc/fedcodec.hip, gfx950 only).
+ * Plain pointers and sizes; every device pointer is caller-owned HBM; every
+ * entry is asynchronous on the given hipStream_t (passed as void*) and never
+ * synchronises, allocates or frees.  Return 0 on success, a negative code on a
+ * rejected argument (message from fc_last_error(), thread-local); no C++
+ * exception crosses the ABI.
+ *
+ * Reference interfaces replaced (file:line under google-research/federated):
+ *   fc_quantize            quantize_utils.uniform_quantize / stochastic_quantize /
+ *                          dithered_quantize (+ generate_noise)
+ *                          aggregators/utils/quantize_utils.py:33-36, 46-53, 57-66
+ *   fc_dequantize          quantize_utils.uniform_dequantize / dithered_dequantize
+ *                          quantize_utils.py:39-42, 69-84; QuantizeEncodeFactory
+ *                          server `dequantize` aggregators/quantize_encode.py:169-171
+ *   fc_quantize_encode     QuantizeEncodeFactory client `quantize` tf_computation
+ *                          quantize_encode.py:139-156 fused with
+ *                          tfc.run_length_gamma_encode (elias_gamma_encode.py:97-99),
+ *                          batched over a round's clients
+ *   fc_rlgamma_encode      tfc.run_length_gamma_encode(int32) (elias_gamma_encode.py:98)
+ *   fc_decode_accumulate   EliasGammaEncodedSumFactory federated_aggregate
+ *                          accumulate/merge (elias_gamma_encode.py:63-88) =
+ *                          tfc.run_length_gamma_decode + int32 sum, optionally fused
+ *                          with the server dequantize (quantize_encode.py:189-190)
+ *   fc_noise_sum           federated_sum(noise) for dithered mode (quantize_encode.py:183)
+ *   fc_client_norms        normalize_fn: mean_magnitude / max_magnitude /
+ *                          dimensionless_norm (quantize_utils.py:20-29,
+ *                          quantize_encode.py:79-90, 145)
+ *   fc_finalize            avg_distortion / avg_sparsity / bit lengths per client
+ *                          (quantize_encode.py:150-155, elias_gamma_encode.py:22-24, 100-108)
+ *   fc_onebit_encode/_decode_sum  OneBitSGDFactory encode/decode_and_sum
+ *                          (comparison_methods/one_bit_sgd.py:45-81, 87-112)
+ *
+ * Bitstream layout (per client): tensorflow-compression run-length gamma
+ * (protocol at elias_gamma_encode.py:30-45), MSB-first within bytes, sign bit 1
+ * = positive; byte length = ceil(bits / 8), last byte zero padded.
+ */
+#ifndef FEDCODEC_H_
+#define FEDCODEC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Rounding modes (QuantizeEncodeFactory rounding_type, quantize_encode.py:92-107). */
+#define FC_UNIFORM 0
+#define FC_STOCHASTIC 1
+#define FC_DITHERED 2
+
+/* Normalisations (quantize_encode.py:79-90). */
+#define FC_NORM_MEAN_MAGNITUDE 1
+#define FC_NORM_MAX_MAGNITUDE 2
+#define FC_NORM_DIMENSIONLESS 3
+
+#define FC_TILE_ELEMS 4096       /* encoder tile = decoder index granularity */
+#define FC_MAX_ELEMS 67108863LL  /* P limit: 2^26 - 1 elements per client tensor */
+
+const char* fc_last_error(void);
+const char* fc_version(void);
+
+/* Number of encoder tiles for P elements: ceil(P / FC_TILE_ELEMS). */
+int64_t fc_num_tiles(int64_t P);
+
+/* Device workspace bytes fc_quantize_encode / fc_rlgamma_encode need for a batch
+ * of `nclients` clients of P elements each.  16-byte aligned pointer required. */
+int64_t fc_encode_workspace_bytes(int32_t nclients, int64_t P);
+
+/* Elementwise quantiser of one tensor: q[i] from x[i] (and noise[i] when
+ * noise != NULL; dithered/stochastic draw the TF stateless_uniform stream of
+ * `seed`).  step is the already-normalised step size. */
+int fc_quantize(const float* x, int64_t P, float step, int64_t seed0, int64_t seed1,
+                int mode, int32_t* q, float* noise, void* stream);
+
+/* Fused client-side quantise + run-length-gamma encode for a batch of clients.
+ *   xs          device array of nclients device pointers to float32[P]
+ *   norms       nullable device float[nclients]: client step = norms[c] * step
+ *   seeds       device int64[2 * nclients] (TF stateless seed per client)
+ *   stream_buf  device byte buffer; client c's code starts at stream_off[c]
+ *               (16-byte aligned) with room for stream_cap[c] bytes
+ *   idx         device uint64[nclients * (fc_num_tiles(P) + 1)]: decoder index
+ *   total_bits  device int64[nclients]: exact code length in bits
+ *   dist_part   device float[nclients * tiles]: per-tile sum (x - deq)^2
+ *   nnz_part    device int32[nclients * tiles]: per-tile nonzero count
+ *   overflow    device int32[nclients]: set to 1 when stream_cap[c] is too small
+ *               (the code is then incomplete; total_bits is still exact)
+ * Bit-exact on q and on the bitstream vs the oracle's restatement. */
+int fc_quantize_encode(const float* const* xs, int32_t nclients, int64_t P, float step,
+                       const float* norms, const int64_t* seeds, int mode,
+                       uint8_t* stream_buf, const int64_t* stream_off,
+                       const int64_t* stream_cap, uint64_t* idx, int64_t* total_bits,
+                       float* dist_part, int32_t* nnz_part, int32_t* overflow,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+
+/* tfc.run_length_gamma_encode over int32 inputs (same batch layout as above,
+ * qs = device array of device pointers to int32[P]). */
+int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P,
+                      uint8_t* stream_buf, const int64_t* stream_off,
+                      const int64_t* stream_cap, uint64_t* idx, int64_t* total_bits,
+                      int32_t* overflow, void* workspace, int64_t workspace_bytes,
+                      void* stream);
+
+/* Decode nclients codes (layout as produced above) and sum them over clients.
+ *   sum_in     nullable int32[P]: running sum to add to (multi-batch rounds)
+ *   sum_out    nullable int32[P]: integer client sum (RCCL all-reduce input)
+ *   out        nullable float[P]: dequantised sum (float(sum) [+ noise_sum]) * step
+ *   noise_sum  nullable float[P] (dithered)
+ *   err        device int32[1]: set nonzero on a malformed stream */
+int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off,
+                         const int64_t* stream_cap, const uint64_t* idx, int32_t nclients,
+                         int64_t P, const int32_t* sum_in, int32_t* sum_out, float* out,
+                         float step, const float* noise_sum, int32_t* err, void* stream);
+
+/* out = (float(sum) [+ noise_sum]) * step (FTZ as TF-CPU). */
+int fc_dequantize(const int32_t* sum, int64_t P, float step, const float* noise_sum,
+                  float* out, void* stream);
+
+/* noise_sum[i] = sum over clients (in client order, float32) of the dither noise
+ * TF's generate_noise(seed_c) draws for element i. */
+int fc_noise_sum(const int64_t* seeds, int32_t nclients, int64_t P, float* noise_sum,
+                 void* stream);
+
+/* norms[c] = normalize_fn(x_c) as float32, for kind in FC_NORM_*. */
+int fc_client_norms(const float* const* xs, int32_t nclients, int64_t P, int kind,
+                    float* norms, void* stream);
+
+/* Per-client reduction of the encoder's per-tile partials:
+ * dist[c] = sum_t dist_part (float64), nnz[c] = sum_t nnz_part (int64). */
+int fc_finalize(const float* dist_part, const int32_t* nnz_part, int32_t nclients, int64_t P,
+                double* dist, int64_t* nnz, void* stream);
+
+/* One-bit SGD (comparison_methods/one_bit_sgd.py): per client the above/below
+ * threshold masks (bit-packed, 1 = x >= threshold), the two means and the
+ * distortion; decode_sum adds every client's decoded tensor in client order. */
+int fc_onebit_encode(const float* const* xs, int32_t nclients, int64_t P, float threshold,
+                     uint32_t* masks, float* means, double* dist, void* stream);
+int fc_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t nclients,
+                         int64_t P, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDCODEC_H_ */

@@ -1,0 +1,149 @@
+"""GPU parity of the HIP codec kernels against the CPU oracle (bit-exact).
+
+Every check goes through the C ABI (federated_amd/_lib.py -> libfedcodec.so).
+"""
+import numpy as np
+import pytest
+import torch
+
+from federated_amd import _lib
+from federated_amd import codec
+from oracle import codec as ocodec
+from oracle import quantize_utils as oq
+
+pytestmark = pytest.mark.gpu
+
+MODES = {"uniform": _lib.UNIFORM, "stochastic": _lib.STOCHASTIC, "dithered": _lib.DITHERED}
+ORACLE_Q = {
+    "uniform": lambda x, s, seed: oq.uniform_quantize(x, s),
+    "stochastic": oq.stochastic_quantize,
+    "dithered": oq.dithered_quantize,
+}
+
+
+def special_values():
+  f32 = np.float32
+  vals = [0.0, -0.0, 1e-45, -1e-45, 1e-39, -1e-39, 1.1754944e-38, -1.1754942e-38, 0.5, -0.5, 1.5,
+          2.5, -2.5, 0.25, 0.75, 1.0, -1.0, 3.0, 1e30, -1e30, np.inf, -np.inf, np.nan, 2.0**31,
+          -2.0**31, 2.0**31 - 128, 2.0**30, -2.0**30 - 64, 1e-20, 7.0, 1e8]
+  return np.array(vals, dtype=f32)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("step", [0.5, 0.4, 1.0 / 127, 1.0, 3.7e-3, 1e-30])
+def test_quantize_matches_oracle(gpu, mode, step):
+  rng = np.random.default_rng(7)
+  x = np.concatenate([rng.standard_normal(20000).astype(np.float32) * 3,
+                      special_values(),
+                      (np.arange(-600, 600, dtype=np.float32) * np.float32(step) * 0.5)])
+  for seed in [(0, 0), (1, 1), (2**40 + 7, 3), (-5, 2**62)]:
+    q, _ = codec.quantize(torch.from_numpy(x).to(gpu), step, seed, MODES[mode])
+    want = ORACLE_Q[mode](x, step, seed)
+    got = q.cpu().numpy()
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (mode, step, seed, x[bad[:5]], got[bad[:5]], want[bad[:5]])
+
+
+def test_noise_matches_oracle(gpu):
+  x = np.zeros(1001, np.float32)
+  _, noise = codec.quantize(torch.from_numpy(x).to(gpu), 1.0, (3, 9), _lib.DITHERED, want_noise=True)
+  np.testing.assert_array_equal(noise.cpu().numpy(), oq.generate_noise((3, 9), 1001))
+
+
+def _rand_q(rng, P, kind):
+  if kind == "sparse":
+    q = rng.integers(-3, 4, P).astype(np.int32)
+    q[rng.random(P) < 0.9] = 0
+  elif kind == "dense":
+    q = np.rint(rng.standard_normal(P) * 3).astype(np.int32)
+  elif kind == "wide":
+    q = (rng.standard_normal(P) * 2.0**rng.integers(0, 30, P)).astype(np.int64)
+    q = np.clip(q, -2**31, 2**31 - 1).astype(np.int32)
+  elif kind == "zeros":
+    q = np.zeros(P, np.int32)
+  elif kind == "runs":
+    q = np.zeros(P, np.int32)
+    pos = rng.choice(P, size=max(1, P // 5000), replace=False)
+    q[pos] = rng.integers(1, 100, pos.size) * rng.choice([-1, 1], pos.size)
+  elif kind == "extreme":
+    q = rng.choice(np.array([-2**31, 2**31 - 1, 1, -1, 0], np.int32), P)
+  else:
+    raise ValueError(kind)
+  return q
+
+
+@pytest.mark.parametrize("P", [1, 3, 4, 5, 1023, 4096, 4099, 20000, 100003])
+@pytest.mark.parametrize("kind", ["sparse", "dense", "wide", "zeros", "runs", "extreme"])
+def test_rlgamma_encode_bytes_match_oracle(gpu, P, kind):
+  rng = np.random.default_rng(P * 31 + len(kind))
+  qs = [_rand_q(rng, P, kind) for _ in range(3)]
+  batch = codec.rlgamma_encode([torch.from_numpy(q).to(gpu) for q in qs])
+  assert not len(codec.check_overflow(batch))
+  bits = batch.bits()
+  for c, q in enumerate(qs):
+    want, nbits = ocodec.run_length_gamma_encode(q)
+    assert bits[c] == nbits
+    assert batch.client_code(c) == want, (c, kind, P)
+  s, _, err = codec.decode_accumulate(batch)
+  assert int(err.item()) == 0
+  want_sum = np.sum(np.stack(qs).astype(np.int64), axis=0)
+  want_sum = ((want_sum + 2**31) % 2**32 - 2**31).astype(np.int32)
+  np.testing.assert_array_equal(s.cpu().numpy(), want_sum)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("P,C", [(1, 2), (4097, 3), (50000, 5), (300000, 7)])
+def test_quantize_encode_batch_matches_oracle(gpu, mode, P, C):
+  rng = np.random.default_rng(P + C)
+  step = 0.5 if mode != "dithered" else 0.3
+  xs = [(rng.standard_normal(P) * rng.uniform(0.1, 2)).astype(np.float32) for _ in range(C)]
+  seeds = np.array([[1000 + c, 77 * c] for c in range(C)], np.int64)
+  batch = codec.quantize_encode_checked([torch.from_numpy(x).to(gpu) for x in xs], step,
+                                        torch.from_numpy(seeds), MODES[mode])
+  bits = batch.bits()
+  acc = np.zeros(P, np.int32)
+  dists, nnzs = codec.finalize(batch)
+  dists = dists.cpu().numpy()
+  nnzs = nnzs.cpu().numpy()
+  noise_sum = np.zeros(P, np.float32)
+  for c in range(C):
+    q = ORACLE_Q[mode](xs[c], step, tuple(seeds[c]))
+    code, nbits = ocodec.run_length_gamma_encode(q)
+    assert bits[c] == nbits
+    assert batch.client_code(c) == code
+    acc = (acc.astype(np.int64) + q).astype(np.int32)
+    if mode == "dithered":
+      n = oq.generate_noise(tuple(seeds[c]), P)
+      noise_sum = noise_sum + n
+      deq = oq.dithered_dequantize(q, step, n)
+    else:
+      deq = oq.uniform_dequantize(q, step)
+    want_d = np.sum((xs[c].astype(np.float64) - deq) ** 2)
+    np.testing.assert_allclose(dists[c], want_d, rtol=1e-5, atol=1e-30)
+    assert nnzs[c] == np.count_nonzero(q)
+  ns = None
+  if mode == "dithered":
+    ns = codec.noise_sum(torch.from_numpy(seeds), P, gpu)
+    np.testing.assert_array_equal(ns.cpu().numpy(), noise_sum)
+  out = torch.empty(P, dtype=torch.float32, device=gpu)
+  s, out, err = codec.decode_accumulate(batch, out=out, step=step, noise_sum=ns)
+  assert int(err.item()) == 0
+  np.testing.assert_array_equal(s.cpu().numpy(), acc)
+  if mode == "dithered":
+    want = oq.dithered_dequantize(acc, step, noise_sum)
+  else:
+    want = oq.uniform_dequantize(acc, step)
+  np.testing.assert_array_equal(out.cpu().numpy(), want)
+
+
+def test_reference_known_answers(gpu):
+  # elias_gamma_encode_test.py:32-37: mean 16 bits; decoded sum = elementwise sum.
+  qs = [np.array([-5, 3, 0, 0], np.int32), np.array([-3, 1, 0, 0], np.int32)]
+  batch = codec.rlgamma_encode([torch.from_numpy(q).to(gpu) for q in qs])
+  assert list(batch.nbytes() * 8) == [16, 16]
+  s, _, _ = codec.decode_accumulate(batch)
+  np.testing.assert_array_equal(s.cpu().numpy(), [-8, 4, 0, 0])
+  # quantize_encode_client_lambda_test.py:93-112 and qsgd_test.py:128-130
+  for q, nbits in (([2, 2, 2], 15), ([1, 1, 1], 9), ([0, 0, 0], 5), ([2, 3, 6], 17)):
+    b = codec.rlgamma_encode([torch.tensor(q, dtype=torch.int32, device=gpu)])
+    assert int(b.bits()[0]) == nbits
