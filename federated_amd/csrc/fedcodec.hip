@@ -19,6 +19,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
+#include <algorithm>
 #include <string>
 
 #include "../../include/fedcodec.h"
@@ -27,7 +29,7 @@ namespace {
 
 constexpr int kTE = FC_TILE_ELEMS;  // elements per tile
 constexpr int kThreads = 256;       // 4 waves of 64
-constexpr int kWinWords = 2048;     // LDS bit window per emission pass (64 Kbit)
+constexpr int kWinWords = 2048;     // LDS bit window (64 Kbit = 16 bits/element)
 constexpr uint32_t kNoPos = 0x1FFF; // "no nonzero" in a 13-bit tile-relative field
 
 // ---------------------------------------------------------------------------
@@ -224,7 +226,7 @@ struct EncodeArgs {
 };
 
 struct EncShared {
-  uint32_t win[kWinWords];
+  uint32_t win[kWinWords];  // LDS bit window (MSB-first words)
   int32_t wave_last[4];
   int32_t wave_first[4];
   uint32_t wave_bits[4];
@@ -232,32 +234,32 @@ struct EncShared {
   int32_t wave_nnz[4];
   uint32_t tail;
   uint32_t ticket;
+  uint32_t next_ticket;
   // look-back results broadcast to the workgroup
   uint64_t b0;
   int32_t last_before;
   uint32_t tail_before;
-  uint32_t r0_R0;      // window bit where the body starts = (b0 % 32) + R0
-  uint32_t nwin_bits;  // bits in the window (incl. trailing code on the last tile)
+  uint32_t r0_R0;      // stream-window bit where the body starts = (b0 % 32) + R0
+  uint32_t nwin_bits;  // bits in the stream window (incl. trailing code on the last tile)
   uint64_t trail;      // trailing run code value
   uint32_t trail_len;
 };
 
-// Emit a piece of <= 32 bits at window bit position wp into the LDS window for
-// pass `pass` (window words [pass*kWinWords, (pass+1)*kWinWords)).
-__device__ __forceinline__ void win_emit32(uint32_t* win, uint32_t v, uint32_t L, uint64_t wp,
-                                           uint64_t pass_lo) {
+// Emit a piece of <= 32 bits at window bit position wp into the LDS window
+// covering window words [pass_lo, pass_lo + kWinWords).
+__device__ __forceinline__ void win_emit32(uint32_t* win, uint32_t v, uint32_t L, uint32_t wp,
+                                           uint32_t pass_lo) {
   if (L == 0) return;
-  const uint64_t w = wp >> 5;
-  const uint32_t o = (uint32_t)(wp & 31);
+  const uint32_t o = wp & 31;
   const uint64_t X = (uint64_t)v << (64 - o - L);
   const uint32_t hi = (uint32_t)(X >> 32), lo = (uint32_t)X;
-  const int64_t i0 = (int64_t)w - (int64_t)pass_lo;
-  if (i0 >= 0 && i0 < kWinWords && hi) atomicOr(&win[i0], hi);
-  if (o + L > 32 && i0 + 1 >= 0 && i0 + 1 < kWinWords && lo) atomicOr(&win[i0 + 1], lo);
+  const int32_t i0 = (int32_t)(wp >> 5) - (int32_t)pass_lo;
+  if ((uint32_t)i0 < (uint32_t)kWinWords && hi) atomicOr(&win[i0], hi);
+  if (o + L > 32 && (uint32_t)(i0 + 1) < (uint32_t)kWinWords && lo) atomicOr(&win[i0 + 1], lo);
 }
 
-__device__ __forceinline__ void win_emit(uint32_t* win, uint64_t v, uint32_t L, uint64_t wp,
-                                         uint64_t pass_lo) {
+__device__ __forceinline__ void win_emit(uint32_t* win, uint64_t v, uint32_t L, uint32_t wp,
+                                         uint32_t pass_lo) {
   if (L > 32) {
     win_emit32(win, (uint32_t)(v >> 32), L - 32, wp, pass_lo);
     win_emit32(win, (uint32_t)v, 32, wp + (L - 32), pass_lo);
@@ -266,115 +268,286 @@ __device__ __forceinline__ void win_emit(uint32_t* win, uint64_t v, uint32_t L, 
   }
 }
 
+// Bits of stream word k covered by a piece (v, L) starting at bit p (MSB-first).
+__device__ __forceinline__ uint32_t piece_word(uint64_t v, uint32_t L, uint32_t p, uint32_t k) {
+  const int32_t lo = 32 * (int32_t)k, end = (int32_t)(p + L);
+  if (L == 0 || end <= lo || (int32_t)p >= lo + 32) return 0;
+  const int32_t sh = lo + 32 - end;
+  return sh >= 0 ? (uint32_t)(sh >= 64 ? 0 : v << sh) : (uint32_t)(-sh >= 64 ? 0 : v >> -sh);
+}
+
 // OR the part of a piece (ending at body position `end`) that falls in the last
 // 32 body bits into the tail word.
-__device__ __forceinline__ void tail_emit(uint32_t* tailw, uint64_t v, uint32_t L, uint64_t end,
-                                          uint64_t body) {
-  const uint64_t s = body - end;
+__device__ __forceinline__ void tail_emit(uint32_t* tailw, uint64_t v, uint32_t L, uint32_t end,
+                                          uint32_t body) {
+  const uint32_t s = body - end;
   if (s < 32 && L) {
     const uint32_t c = (uint32_t)(v << s);
     if (c) atomicOr(tailw, c);
   }
 }
 
+__device__ __forceinline__ Seg seg_identity() {
+  Seg s;
+  s.has_nz = 0;
+  s.first = s.last = 0;
+  s.body = 0;
+  s.tail = 0;
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// DPP wavefront scans (GFX9 row_shr / row_bcast / wave_shr; VALU, no LDS).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t dpp_incl_sum(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+__device__ __forceinline__ int32_t dpp_incl_max(int32_t x) {
+  const int32_t id = (int32_t)0x80000000;
+  x = max(x, __builtin_amdgcn_update_dpp(id, x, 0x111, 0xf, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(id, x, 0x112, 0xf, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(id, x, 0x114, 0xf, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(id, x, 0x118, 0xf, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(id, x, 0x142, 0xa, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(id, x, 0x143, 0xc, 0xf, false));
+  return x;
+}
+__device__ __forceinline__ int32_t dpp_shr1(int32_t x, int32_t fill) {  // wave_shr:1
+  return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int32_t lane63(int32_t x) { return __builtin_amdgcn_readlane(x, 63); }
+
+// Decoupled look-back for tile t of one client, run by one full wave.  Returns
+// the exclusive prefix (a root segment: body = stream bits before tile t).
+__device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int lane,
+                                        uint32_t* spin_err) {
+  Seg S = seg_identity();
+  int64_t base = (int64_t)t - 1;
+  for (;;) {
+    const int64_t ti = base - lane;
+    uint64_t w1 = kFlagPre, w2 = kFlagPre;  // ti < 0: virtual root prefix
+    bool valid = ti < 0;
+    int k;
+    uint32_t spins = 0;
+    for (;;) {
+      if (!valid) {
+        w1 = ld_agent(status_c + 2 * ti);
+        w2 = ld_agent(status_c + 2 * ti + 1);
+        valid = (w1 >> 62) != 0 && (w1 >> 62) == (w2 >> 62);
+      }
+      const uint64_t pre = __ballot(valid && (w1 >> 62) == 2);
+      const uint64_t val = __ballot(valid);
+      k = pre ? __builtin_ctzll(pre) : 64;
+      const uint64_t need = k >= 63 ? ~0ull : ((2ull << k) - 1);
+      if ((val & need) == need) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) {  // safety net only: tickets guarantee progress
+        if (lane == 0) atomicOr(spin_err, 1u);
+        k = 0;
+        w1 = kFlagPre;
+        w2 = kFlagPre;
+        break;
+      }
+    }
+    Seg v = (lane <= k && ti >= -1) ? seg_from_status(w1, w2, ti * kTE) : seg_identity();
+    // suffix scan over lanes 0..k: lane 0 ends with the combination of the window
+    const int kk = k < 63 ? k : 63;
+    for (int d = 1; d <= kk; d <<= 1) {
+      Seg o;
+      o.has_nz = __shfl_down(v.has_nz, d, 64);
+      o.first = __shfl_down(v.first, d, 64);
+      o.last = __shfl_down(v.last, d, 64);
+      o.body = __shfl_down(v.body, d, 64);
+      o.tail = __shfl_down(v.tail, d, 64);
+      if (lane + d >= 64) o.has_nz = 0;
+      v = seg_combine(o, v);
+    }
+    Seg W;
+    W.has_nz = __builtin_amdgcn_readfirstlane(v.has_nz);
+    W.first = __builtin_amdgcn_readfirstlane(v.first);
+    W.last = __builtin_amdgcn_readfirstlane(v.last);
+    W.body = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v.body >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)v.body);
+    W.tail = __builtin_amdgcn_readfirstlane(v.tail);
+    S = seg_combine(W, S);
+    if (k < 64) break;
+    base -= 64;
+  }
+  return S;
+}
+
+// Raw 4x4 input words (float or int32 bit patterns) of one thread's chunks.
+template <bool INT_IN>
+__device__ __forceinline__ void load_raw(const EncodeArgs& a, uint32_t ticket, int wv, int lane,
+                                         uint32_t (&raw)[4][4]) {
+  const int32_t t = (int32_t)(ticket / (uint32_t)a.nclients);
+  const int32_t c = (int32_t)(ticket - (uint32_t)t * (uint32_t)a.nclients);
+  const int64_t tile_base = (int64_t)t * kTE;
+  const uint32_t* xp = (const uint32_t*)a.xs[c];
+  const bool aligned = (((uintptr_t)xp) & 15) == 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t e0 = tile_base + 1024 * wv + 256 * j + 4 * lane;
+    if (aligned && e0 + 3 < a.P) {
+      const uint4 v = *(const uint4*)(xp + e0);
+      raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) raw[j][k] = (e0 + k < a.P) ? xp[e0 + k] : 0u;
+    }
+  }
+}
+
+struct ClientQ {
+  float step;
+  Key4 key;
+};
+
 template <int MODE, bool INT_IN>
-__global__ __launch_bounds__(kThreads) void k_encode(EncodeArgs a) {
+__device__ __forceinline__ ClientQ client_q(const EncodeArgs& a, int32_t c) {
+  ClientQ r;
+  r.step = a.step;
+  if (!INT_IN && a.norms) r.step = a.norms[c] * a.step;
+  r.key = Key4{0, 0, 0, 0};
+  if (!INT_IN && MODE != FC_UNIFORM) r.key = tf_seed_scramble(a.seeds[2 * c], a.seeds[2 * c + 1]);
+  return r;
+}
+
+// Quantise one chunk of 4 consecutive elements starting at e0.
+template <int MODE, bool INT_IN>
+__device__ __forceinline__ void quant_chunk(const ClientQ& cq, int64_t e0, int64_t P,
+                                            const uint32_t (&r4)[4], int32_t (&q4)[4],
+                                            float& dist) {
+  if (INT_IN) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q4[k] = (int32_t)r4[k];
+  } else {
+    uint4 rb = make_uint4(0, 0, 0, 0);
+    if (MODE != FC_UNIFORM) rb = philox_group(cq.key, (uint32_t)(e0 >> 2));
+    const uint32_t rr[4] = {rb.x, rb.y, rb.z, rb.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float deq, noise;
+      const float xv = __uint_as_float(r4[k]);
+      const int32_t qq = quantize_one<MODE>(xv, cq.step, rr[k], deq, noise);
+      const bool valid = e0 + k < P;
+      q4[k] = valid ? qq : 0;
+      const float dd = xv - deq;
+      dist += valid ? dd * dd : 0.0f;
+    }
+  }
+}
+
+template <int MODE, bool INT_IN>
+__device__ __forceinline__ void quantize_raw(const EncodeArgs& a, int32_t c, int64_t tile_base,
+                                             int wv, int lane, const uint32_t (&raw)[4][4],
+                                             int32_t (&q)[4][4], float& dist) {
+  const ClientQ cq = client_q<MODE, INT_IN>(a, c);
+  dist = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t e0 = tile_base + 1024 * wv + 256 * j + 4 * lane;
+    quant_chunk<MODE, INT_IN>(cq, e0, a.P, raw[j], q[j], dist);
+  }
+}
+
+#ifdef FC_STAMPS
+__device__ unsigned long long g_stamps[8];
+#define STAMP(i)                                               \
+  do {                                                         \
+    if (tid == 0) {                                            \
+      const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
+      st_acc[i] += now_ - st_last;                             \
+      st_last = now_;                                          \
+    }                                                          \
+  } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#endif
+
+template <int MODE, bool INT_IN>
+__global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
   __shared__ EncShared sh;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
   const uint32_t total_tiles = (uint32_t)a.nclients * (uint32_t)a.T;
+#ifdef FC_STAMPS
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int i = tid; i < kWinWords; i += kThreads) sh.win[i] = 0;
+  if (tid == 0) sh.ticket = atomicAdd(a.counter, 1u);
+  __syncthreads();
+  uint32_t ticket = sh.ticket;
+  uint32_t raw[4][4];
+  if (ticket < total_tiles) load_raw<INT_IN>(a, ticket, wv, lane, raw);
 
-  for (;;) {
-    if (tid == 0) sh.ticket = atomicAdd(a.counter, 1u);
-    __syncthreads();
-    const uint32_t ticket = sh.ticket;
-    if (ticket >= total_tiles) break;
-    const int32_t c = (int32_t)(ticket / (uint32_t)a.T);
-    const int32_t t = (int32_t)(ticket - (uint32_t)c * (uint32_t)a.T);
+  while (ticket < total_tiles) {
+    STAMP(0);
+    if (tid == 0) {
+      sh.next_ticket = atomicAdd(a.counter, 1u);  // read after the first barrier
+      sh.tail = 0;
+    }
+    // tickets interleave clients (tile-major) so each client has few tiles in
+    // flight and the look-back almost always finds a prefix at distance 1
+    const int32_t t = (int32_t)(ticket / (uint32_t)a.nclients);
+    const int32_t c = (int32_t)(ticket - (uint32_t)t * (uint32_t)a.nclients);
     const int64_t P = a.P;
     const int64_t tile_base = (int64_t)t * kTE;
     const bool last_tile = (t == a.T - 1);
 
-    // ---- load + quantise: thread owns 4 chunks of 4 consecutive elements ----
+    // ---- phase A: quantise (thread owns 4 chunks of 4 consecutive elements) ----
     int32_t q[4][4];
-    float dist = 0.0f;
-    int32_t nnz = 0;
-    {
-      float step = a.step;
-      if (!INT_IN && a.norms) step = a.norms[c] * a.step;
-      Key4 key{0, 0, 0, 0};
-      if (!INT_IN && MODE != FC_UNIFORM) key = tf_seed_scramble(a.seeds[2 * c], a.seeds[2 * c + 1]);
-      const void* xp = a.xs[c];
-      const bool aligned = (((uintptr_t)xp) & 15) == 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t e0 = tile_base + 1024 * wv + 256 * j + 4 * lane;
-        if (INT_IN) {
-          const int32_t* qp = (const int32_t*)xp;
-          if (aligned && e0 + 3 < P) {
-            const int4 v = *(const int4*)(qp + e0);
-            q[j][0] = v.x; q[j][1] = v.y; q[j][2] = v.z; q[j][3] = v.w;
-          } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) q[j][k] = (e0 + k < P) ? qp[e0 + k] : 0;
-          }
-        } else {
-          const float* fp = (const float*)xp;
-          float xv[4];
-          if (aligned && e0 + 3 < P) {
-            const float4 v = *(const float4*)(fp + e0);
-            xv[0] = v.x; xv[1] = v.y; xv[2] = v.z; xv[3] = v.w;
-          } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) xv[k] = (e0 + k < P) ? fp[e0 + k] : 0.0f;
-          }
-          uint4 rb = make_uint4(0, 0, 0, 0);
-          if (MODE != FC_UNIFORM) rb = philox_group(key, (uint32_t)(e0 >> 2));
-          const uint32_t rr[4] = {rb.x, rb.y, rb.z, rb.w};
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            float deq, noise;
-            const int32_t qq = quantize_one<MODE>(xv[k], step, rr[k], deq, noise);
-            const bool valid = e0 + k < P;
-            q[j][k] = valid ? qq : 0;
-            const float dd = xv[k] - deq;
-            dist += valid ? dd * dd : 0.0f;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) nnz += q[j][k] != 0;
-      }
-    }
+    float dist;
+    quantize_raw<MODE, INT_IN>(a, c, tile_base, wv, lane, raw, q, dist);
+    STAMP(1);
 
-    // ---- max-scan of nonzero positions (tile-relative), wave level ----
-    int32_t chunk_prev[4];  // last nonzero before this chunk within the wave, or -1
-    int32_t carry = -1, wfirst = 0x7FFFFFFF;
+    // ---- phase B: max-scan of nonzero positions (tile-relative) ----
+    int32_t chunk_prev[4];  // last nonzero before the chunk, or -1
+    int32_t carry = -1, wfirst = 0x7FFFFFFF, nnz = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-      int32_t cl = -1, cf = 0x7FFFFFFF;
+      int32_t cl = -1;
 #pragma unroll
-      for (int k = 3; k >= 0; --k)
-        if (q[j][k] != 0) cf = rel0 + k;
+      for (int k = 3; k >= 0; --k) {
+        nnz += q[j][k] != 0;
+        if (q[j][k] != 0) wfirst = min(wfirst, rel0 + k);
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (q[j][k] != 0) cl = rel0 + k;
-      wfirst = min(wfirst, cf);
-      const int32_t incl = wave_incl_max(cl, lane);
-      int32_t excl = __shfl_up(incl, 1, 64);
-      if (lane == 0) excl = -1;
-      chunk_prev[j] = max(excl, carry);
-      carry = max(carry, __shfl(incl, 63, 64));
+      const int32_t incl = dpp_incl_max(cl);
+      chunk_prev[j] = max(dpp_shr1(incl, -1), carry);
+      carry = max(carry, lane63(incl));
     }
-    wfirst = wave_min(wfirst);
-    if (lane == 0) {
-      sh.wave_last[wv] = carry;
-      sh.wave_first[wv] = wfirst;
+    {
+      float d = dist;
+      int32_t n = nnz;
+      int32_t f = wfirst;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        d += __shfl_xor(d, o, 64);
+        n += __shfl_xor(n, o, 64);
+        f = min(f, __shfl_xor(f, o, 64));
+      }
+      if (lane == 0) {
+        sh.wave_dist[wv] = d;
+        sh.wave_nnz[wv] = n;
+        sh.wave_last[wv] = carry;
+        sh.wave_first[wv] = f;
+      }
     }
     __syncthreads();
+    STAMP(2);
     int32_t wave_in = -1;
     for (int w = 0; w < wv; ++w) wave_in = max(wave_in, sh.wave_last[w]);
     int32_t tile_first = 0x7FFFFFFF, tile_last = -1;
@@ -383,14 +556,22 @@ __global__ __launch_bounds__(kThreads) void k_encode(EncodeArgs a) {
       tile_first = min(tile_first, sh.wave_first[w]);
       tile_last = max(tile_last, sh.wave_last[w]);
     }
+    if (tid == 0) {
+      const float d = ((sh.wave_dist[0] + sh.wave_dist[1]) + sh.wave_dist[2]) + sh.wave_dist[3];
+      const int32_t n = sh.wave_nnz[0] + sh.wave_nnz[1] + sh.wave_nnz[2] + sh.wave_nnz[3];
+      if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
+      if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t] = n;
+    }
+    const uint32_t next = sh.next_ticket;
 
-    // ---- code lengths of the body and wave-level sum-scan ----
+    // ---- phase C: body code lengths, sum-scan ----
     uint32_t chunk_off[4];
     uint32_t wbits = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      chunk_prev[j] = max(chunk_prev[j], wave_in);
       const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-      int32_t prev = max(chunk_prev[j], wave_in);
+      int32_t prev = chunk_prev[j];
       uint32_t bits = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -401,77 +582,107 @@ __global__ __launch_bounds__(kThreads) void k_encode(EncodeArgs a) {
           prev = rel0 + k;
         }
       }
-      const uint32_t incl = wave_incl_sum(bits, lane);
+      const uint32_t incl = dpp_incl_sum(bits);
       chunk_off[j] = wbits + incl - bits;
-      wbits += __shfl(incl, 63, 64);
+      wbits += (uint32_t)lane63((int32_t)incl);
     }
     if (lane == 0) sh.wave_bits[wv] = wbits;
-    // per-wave measurement partials
-    {
-      float d = dist;
-      int32_t n = nnz;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        d += __shfl_xor(d, o, 64);
-        n += __shfl_xor(n, o, 64);
-      }
-      if (lane == 0) {
-        sh.wave_dist[wv] = d;
-        sh.wave_nnz[wv] = n;
-      }
-    }
-    if (tid == 0) sh.tail = 0;
     __syncthreads();
+    STAMP(3);
     uint32_t woff = 0, body = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       woff += (w < wv) ? sh.wave_bits[w] : 0u;
       body += sh.wave_bits[w];
     }
-    if (tid == 0) {
-      const float d = ((sh.wave_dist[0] + sh.wave_dist[1]) + sh.wave_dist[2]) + sh.wave_dist[3];
-      const int32_t n = sh.wave_nnz[0] + sh.wave_nnz[1] + sh.wave_nnz[2] + sh.wave_nnz[3];
-      if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
-      if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t] = n;
-    }
+    // fast path: the whole body (+ trailing code + one funnel word) fits the window
+    const bool fast = body + 64u <= 32u * (kWinWords - 1);
 
-    // ---- tail: last 32 bits of the body ----
+    // ---- phase D: emit the body at body-relative bit offsets (fast path) or
+    //      just its last 32 bits (slow path); then prefetch the next tile ----
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t off = woff + chunk_off[j];
-      if (off + 4 * 89 + 32 < body) continue;  // cannot reach the last 32 bits
+      if (!fast && off + 4 * 89 + 32 < body) continue;
       const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-      int32_t prev = max(chunk_prev[j], wave_in);
-      uint64_t pos = off;
+      int32_t prev = chunk_prev[j];
+      uint32_t pos = off;
+      uint64_t acc = 0;  // pending bits of this chunk (fast path)
+      uint32_t nacc = 0, accpos = off;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int32_t v = q[j][k];
         if (v == 0) continue;
-        if (prev >= 0) {
-          const uint32_t d = (uint32_t)(rel0 + k - prev);
-          const uint32_t rl = glen(d);
-          pos += rl;
-          tail_emit(&sh.tail, d, rl, pos, body);
-        }
         const uint32_t m = mag_u32(v);
         const uint32_t ml = glen(m);
         const uint64_t sm = ((uint64_t)(v > 0) << ml) | m;
-        pos += 1 + ml;
-        tail_emit(&sh.tail, sm, 1 + ml, pos, body);
+        uint64_t code;
+        uint32_t L;
+        if (prev >= 0) {
+          const uint32_t d = (uint32_t)(rel0 + k - prev);
+          const uint32_t rl = glen(d);
+          L = rl + 1 + ml;
+          if (L <= 64) {
+            code = ((uint64_t)d << (1 + ml)) | sm;
+          } else {  // rare: > 64-bit code, emit the run code on its own
+            if (fast) {
+              if (nacc) win_emit(sh.win, acc, nacc, accpos, 0);
+              win_emit(sh.win, d, rl, pos, 0);
+              acc = 0;
+              nacc = 0;
+            } else {
+              tail_emit(&sh.tail, d, rl, pos + rl, body);
+            }
+            pos += rl;
+            accpos = pos;
+            code = sm;
+            L = 1 + ml;
+          }
+        } else {
+          code = sm;
+          L = 1 + ml;
+        }
+        if (fast) {
+          if (nacc + L > 64) {
+            win_emit(sh.win, acc, nacc, accpos, 0);
+            acc = 0;
+            nacc = 0;
+            accpos = pos;
+          }
+          acc = (L >= 64 ? 0 : acc << L) | code;
+          nacc += L;
+        } else {
+          tail_emit(&sh.tail, code, L, pos + L, body);
+        }
+        pos += L;
         prev = rel0 + k;
       }
+      if (fast && nacc) win_emit(sh.win, acc, nacc, accpos, 0);
     }
+    if (next < total_tiles) load_raw<INT_IN>(a, next, wv, lane, raw);
     __syncthreads();
+    STAMP(4);
 
-    // ---- publish aggregate, decoupled look-back (wave 0) ----
-    uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t);
+    // ---- phase E: publish aggregate, decoupled look-back (wave 0) ----
     if (wv == 0) {
+      uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t);
       Seg agg;
       agg.has_nz = tile_last >= 0;
       agg.first = agg.has_nz ? (int32_t)(tile_base + tile_first) : 0;
       agg.last = agg.has_nz ? (int32_t)(tile_base + tile_last) : 0;
       agg.body = body;
-      agg.tail = sh.tail;
+      if (fast) {
+        uint32_t tl = 0;
+        if (body >= 32) {
+          const uint32_t s = body - 32, w = s >> 5, o = s & 31;
+          tl = o ? (sh.win[w] << o) | (sh.win[w + 1] >> (32 - o)) : sh.win[w];
+        } else if (body) {
+          tl = sh.win[0] >> (32 - body);
+        }
+        agg.tail = tl;
+      } else {
+        agg.tail = sh.tail;
+      }
       Seg excl;
       if (t == 0) {
         excl.has_nz = 1;
@@ -486,68 +697,8 @@ __global__ __launch_bounds__(kThreads) void k_encode(EncodeArgs a) {
           st_agent(st + 1, kFlagAgg | agg.tail);
           st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
         }
-        Seg S;
-        S.has_nz = 0;
-        S.first = S.last = 0;
-        S.body = 0;
-        S.tail = 0;
-        int64_t base = (int64_t)t - 1;
-        for (;;) {
-          const int64_t ti = base - lane;
-          uint64_t w1 = kFlagPre, w2 = kFlagPre;  // ti < 0: virtual root prefix
-          if (ti >= 0) {
-            const uint64_t* sp = a.status + 2 * ((int64_t)c * a.T + ti);
-            uint32_t spins = 0;
-            for (;;) {
-              w1 = ld_agent(sp);
-              w2 = ld_agent(sp + 1);
-              if ((w1 >> 62) != 0 && (w1 >> 62) == (w2 >> 62)) break;
-              __builtin_amdgcn_s_sleep(1);
-              if (++spins > (1u << 26)) {
-                atomicOr(a.spin_err, 1u);
-                w1 = kFlagPre;
-                w2 = kFlagPre;
-                break;
-              }
-            }
-          }
-          const bool is_pre = (w1 >> 62) == 2;
-          const uint64_t pm = __ballot(is_pre);
-          const int k = pm ? __builtin_ctzll(pm) : 64;
-          Seg v;
-          if (lane <= k && ti >= -1) {
-            v = seg_from_status(w1, w2, ti * kTE);
-          } else {
-            v.has_nz = 0;
-            v.first = v.last = 0;
-            v.body = 0;
-            v.tail = 0;
-          }
-          // suffix scan: lane l <- combine(lanes [l+d ...], lane l)
-#pragma unroll
-          for (int d = 1; d < 64; d <<= 1) {
-            Seg o;
-            o.has_nz = __shfl_down(v.has_nz, d, 64);
-            o.first = __shfl_down(v.first, d, 64);
-            o.last = __shfl_down(v.last, d, 64);
-            o.body = __shfl_down(v.body, d, 64);
-            o.tail = __shfl_down(v.tail, d, 64);
-            if (lane + d >= 64) o.has_nz = 0;
-            v = seg_combine(o, v);
-          }
-          Seg W;
-          W.has_nz = __shfl(v.has_nz, 0, 64);
-          W.first = __shfl(v.first, 0, 64);
-          W.last = __shfl(v.last, 0, 64);
-          W.body = __shfl(v.body, 0, 64);
-          W.tail = __shfl(v.tail, 0, 64);
-          S = seg_combine(W, S);
-          if (k < 64) break;
-          base -= 64;
-        }
-        excl = S;
+        excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, a.spin_err);
       }
-      // excl is a root segment: body = stream bits before this tile.
       const Seg incl = seg_combine(excl, agg);
       if (lane == 0) {
         st_agent(st + 1, kFlagPre | incl.tail);
@@ -561,7 +712,6 @@ __global__ __launch_bounds__(kThreads) void k_encode(EncodeArgs a) {
         uint32_t R0 = 0;
         if (agg.has_nz) R0 = glen((uint32_t)(agg.first - excl.last));
         sh.r0_R0 = r0 + R0;
-        uint64_t nbits = (uint64_t)r0 + R0 + body;
         uint32_t tl = 0;
         uint64_t tv = 0;
         if (last_tile) {
@@ -569,80 +719,116 @@ __global__ __launch_bounds__(kThreads) void k_encode(EncodeArgs a) {
           if (zc > 0) {
             tv = (uint64_t)(zc + 1);
             tl = 2u * (63u - (uint32_t)__clzll(tv)) + 1u;
+            if (fast) win_emit(sh.win, tv, tl, body, 0);  // body-relative
           }
           a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
           a.total_bits[c] = (int64_t)incl.body + tl;
         }
         sh.trail = tv;
         sh.trail_len = tl;
-        sh.nwin_bits = (uint32_t)(nbits + tl);
+        sh.nwin_bits = r0 + R0 + body + tl;
       }
     }
     __syncthreads();
+    STAMP(5);
 
-    // ---- emit the code into the LDS window, then store owned words ----
+    // ---- phase F: store the words this tile owns ----
     const uint64_t b0 = sh.b0;
     const uint32_t bstart = sh.r0_R0;
     const uint32_t nwin_bits = sh.nwin_bits;
     const int32_t last_before = sh.last_before;
     const uint32_t nwords_owned = last_tile ? (nwin_bits + 31) / 32 : nwin_bits / 32;
-    const uint32_t npass = (nwords_owned + kWinWords - 1) / kWinWords;
     const int64_t cap = a.stream_cap[c];
     uint32_t* out32 = (uint32_t*)(a.stream_buf + a.stream_off[c]);
     const uint64_t w0 = b0 >> 5;
+    const uint32_t r0 = (uint32_t)(b0 & 31);
     if (tid == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&a.overflow[c], 1u);
-    for (uint32_t pass = 0; pass < npass; ++pass) {
-      const uint64_t plo = (uint64_t)pass * kWinWords;
-      if (tid == 0) {
-        const uint32_t r0 = (uint32_t)(b0 & 31);
-        if (r0) win_emit32(sh.win, sh.tail_before & ((1u << r0) - 1u), r0, 0, plo);
-        if (tile_last >= 0) {
-          const uint32_t d = (uint32_t)(tile_base + tile_first - last_before);
-          win_emit(sh.win, d, glen(d), r0, plo);
+    if (fast) {
+      const uint32_t dfirst = tile_last >= 0 ? (uint32_t)(tile_base + tile_first - last_before) : 0u;
+      const uint32_t R0 = bstart - r0;
+      const uint32_t tb = sh.tail_before & (r0 ? ((1u << r0) - 1u) : 0u);
+      for (uint32_t k = tid; k < nwords_owned; k += kThreads) {
+        // stream-window bits [32k, 32k+32) = body bits [32k - bstart, ...)
+        const int32_t s = 32 * (int32_t)k - (int32_t)bstart;
+        uint32_t wv32;
+        if (s >= 0) {
+          const uint32_t w = (uint32_t)s >> 5, o = (uint32_t)s & 31;
+          wv32 = o ? (sh.win[w] << o) | (sh.win[w + 1] >> (32 - o)) : sh.win[w];
+        } else {
+          wv32 = (-s < 32) ? (sh.win[0] >> -s) : 0u;
+          wv32 |= piece_word(tb, r0, 0, k) | piece_word(dfirst, R0, r0, k);
         }
-        if (sh.trail_len) win_emit(sh.win, sh.trail, sh.trail_len, (uint64_t)bstart + body, plo);
+        if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
       }
+      __syncthreads();
+      const uint32_t nt = min((uint32_t)kWinWords, (body + sh.trail_len + 31) / 32 + 1);
+      for (uint32_t i = tid; i < nt; i += kThreads) sh.win[i] = 0;
+    } else {
+      // slow path (codes > 16 bits/element on average): re-read and re-quantise
+      // this tile one chunk at a time and emit stream-relative in window passes
+      const ClientQ cq = client_q<MODE, INT_IN>(a, c);
+      const uint32_t* xp = (const uint32_t*)a.xs[c];
+      const uint32_t npass = (nwords_owned + kWinWords - 1) / kWinWords;
+      for (uint32_t pass = 0; pass < npass; ++pass) {
+        const uint32_t plo = pass * kWinWords;
+        if (tid == 0) {
+          if (r0) win_emit32(sh.win, sh.tail_before & ((1u << r0) - 1u), r0, 0, plo);
+          if (tile_last >= 0) {
+            const uint32_t d = (uint32_t)(tile_base + tile_first - last_before);
+            win_emit(sh.win, d, glen(d), r0, plo);
+          }
+          if (sh.trail_len) win_emit(sh.win, sh.trail, sh.trail_len, bstart + body, plo);
+        }
+#pragma unroll 1
+        for (int j = 0; j < 4; ++j) {
+          const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
+          const int64_t e0 = tile_base + rel0;
+          int32_t prev = j == 0 ? chunk_prev[0] : j == 1 ? chunk_prev[1] : j == 2 ? chunk_prev[2] : chunk_prev[3];
+          uint32_t pos = bstart + woff +
+                         (j == 0 ? chunk_off[0] : j == 1 ? chunk_off[1] : j == 2 ? chunk_off[2] : chunk_off[3]);
+          uint32_t r4[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-        int32_t prev = max(chunk_prev[j], wave_in);
-        uint64_t pos = (uint64_t)bstart + woff + chunk_off[j];
+          for (int k = 0; k < 4; ++k) r4[k] = (e0 + k < P) ? xp[e0 + k] : 0u;
+          int32_t q4[4];
+          float dd = 0.0f;
+          quant_chunk<MODE, INT_IN>(cq, e0, P, r4, q4, dd);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int32_t v = q[j][k];
-          if (v == 0) continue;
-          const uint32_t m = mag_u32(v);
-          const uint32_t ml = glen(m);
-          const uint64_t sm = ((uint64_t)(v > 0) << ml) | m;
-          if (prev >= 0) {
-            const uint32_t d = (uint32_t)(rel0 + k - prev);
-            const uint32_t rl = glen(d);
-            if (rl + 1 + ml <= 32) {
-              win_emit32(sh.win, (uint32_t)(((uint64_t)d << (1 + ml)) | sm), rl + 1 + ml, pos, plo);
-            } else {
+          for (int k = 0; k < 4; ++k) {
+            const int32_t v = q4[k];
+            if (v == 0) continue;
+            const uint32_t m = mag_u32(v);
+            const uint32_t ml = glen(m);
+            const uint64_t sm = ((uint64_t)(v > 0) << ml) | m;
+            if (prev >= 0) {
+              const uint32_t d = (uint32_t)(rel0 + k - prev);
+              const uint32_t rl = glen(d);
               win_emit32(sh.win, d, rl, pos, plo);
-              win_emit(sh.win, sm, 1 + ml, pos + rl, plo);
+              pos += rl;
             }
-            pos += rl + 1 + ml;
-          } else {
             win_emit(sh.win, sm, 1 + ml, pos, plo);
             pos += 1 + ml;
+            prev = rel0 + k;
           }
-          prev = rel0 + k;
         }
+        __syncthreads();
+        const uint32_t nw = min((uint32_t)kWinWords, nwords_owned - plo);
+        for (uint32_t i = tid; i < nw; i += kThreads) {
+          const uint64_t wi = w0 + plo + i;
+          if ((int64_t)(wi + 1) * 4 <= cap) out32[wi] = bswap32(sh.win[i]);
+        }
+        __syncthreads();
+        const uint32_t nt = min((uint32_t)kWinWords, (nwin_bits + 31) / 32 - plo);
+        for (uint32_t i = tid; i < nt; i += kThreads) sh.win[i] = 0;
+        __syncthreads();
       }
-      __syncthreads();
-      const uint32_t nw = min((uint32_t)kWinWords, nwords_owned - pass * kWinWords);
-      for (uint32_t i = tid; i < nw; i += kThreads) {
-        const uint64_t wi = w0 + plo + i;
-        if ((int64_t)(wi + 1) * 4 <= cap) out32[wi] = bswap32(sh.win[i]);
-      }
-      __syncthreads();
-      for (uint32_t i = tid; i < kWinWords; i += kThreads) sh.win[i] = 0;
-      // the next ticket's __syncthreads (or the next pass's) orders this clear
-      if (pass + 1 < npass) __syncthreads();
     }
+    STAMP(6);
+    ticket = next;
   }
+#ifdef FC_STAMPS
+  if (tid == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_stamps[i], (unsigned long long)st_acc[i]);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1058,7 +1244,10 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t total = (int64_t)nclients * T;
-  const int grid = (int)std::min<int64_t>(total, (int64_t)ncu * 8);
+  // few clients: cap the tiles in flight per client so look-back windows stay short
+  int64_t max_grid = std::min<int64_t>((int64_t)ncu * 8, std::max<int64_t>(128, 64LL * nclients));
+  if (const char* g = getenv("FEDCODEC_ENC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
+  const int grid = (int)std::min<int64_t>(total, max_grid);
   if (int_in) {
     hipLaunchKernelGGL((k_encode<FC_UNIFORM, true>), dim3(grid), dim3(kThreads), 0, s, a);
   } else if (mode == FC_UNIFORM) {
@@ -1077,6 +1266,16 @@ extern "C" {
 
 const char* fc_last_error(void) { return g_err.c_str(); }
 const char* fc_version(void) { return "fedcodec 0.1 gfx950"; }
+#ifdef FC_STAMPS
+int fc_debug_stamps(unsigned long long* host8, int reset) {
+  if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 int64_t fc_num_tiles(int64_t P) { return P <= 0 ? 0 : tiles_for(P); }
 int64_t fc_encode_workspace_bytes(int32_t nclients, int64_t P) {
   if (nclients <= 0 || P <= 0) return 256;

@@ -147,3 +147,27 @@ def test_reference_known_answers(gpu):
   for q, nbits in (([2, 2, 2], 15), ([1, 1, 1], 9), ([0, 0, 0], 5), ([2, 3, 6], 17)):
     b = codec.rlgamma_encode([torch.tensor(q, dtype=torch.int32, device=gpu)])
     assert int(b.bits()[0]) == nbits
+
+
+@pytest.mark.parametrize("grid", ["1", "5", "64"])
+def test_encode_many_tiles_per_workgroup(gpu, grid, monkeypatch):
+  """Persistent workgroups that each take many tiles (LDS window reuse) and a
+  look-back that crosses many tiles (grid 64 over 2 x 245 tiles)."""
+  monkeypatch.setenv("FEDCODEC_ENC_GRID", grid)
+  rng = np.random.default_rng(int(grid))
+  P, C = 1_000_003, 2
+  xs = [(rng.standard_normal(P) * 0.7).astype(np.float32) for _ in range(C)]
+  xs[1][100_000:900_000] = 0.0  # long zero runs crossing many tiles
+  seeds = np.array([[5, 6], [7, 8]], np.int64)
+  batch = codec.quantize_encode_checked([torch.from_numpy(x).to(gpu) for x in xs], 0.25,
+                                        torch.from_numpy(seeds), _lib.STOCHASTIC)
+  acc = np.zeros(P, np.int64)
+  for c in range(C):
+    q = oq.stochastic_quantize(xs[c], 0.25, tuple(seeds[c]))
+    code, nbits = ocodec.run_length_gamma_encode(q)
+    assert int(batch.bits()[c]) == nbits
+    assert batch.client_code(c) == code
+    acc += q
+  s, _, err = codec.decode_accumulate(batch)
+  assert int(err.item()) == 0
+  np.testing.assert_array_equal(s.cpu().numpy(), acc.astype(np.int32))

@@ -1,0 +1,43 @@
+"""Diagnostic: per-phase cycle shares of k_encode (FC_STAMPS build).
+
+FEDCODEC_LIB=federated_amd/libfedcodec_stamps.so python tools/stamps.py
+"""
+import ctypes
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from federated_amd import _lib, codec  # noqa: E402
+
+P = int(os.environ.get("P", 25_000_000))
+C = int(os.environ.get("C", 128))
+mode = int(os.environ.get("MODE", _lib.STOCHASTIC))
+lib = _lib.load()
+lib.fc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev)
+g.manual_seed(1)
+pool = [torch.randn(P, generator=g, device=dev) for _ in range(4)]
+rows = [pool[c % 4] for c in range(C)]
+ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
+batch = codec.EncodedBatch(P, C, [P + 1024] * C, dev)
+buf = (ctypes.c_ulonglong * 8)()
+for it in range(3):
+  lib.fc_debug_stamps(buf, 1)
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  codec.quantize_encode(None, 0.5, seeds, mode, ptrs=ptrs, P=P, out=batch)
+  torch.cuda.synchronize()
+  dt = time.perf_counter() - t0
+  lib.fc_debug_stamps(buf, 0)
+tiles = C * codec.num_tiles(P)
+names = ["ticket+barrier", "A load+quantize", "B maxscan+barrier", "C lengths+barrier",
+         "D tail+barrier", "E lookback+barrier", "F emit+store"]
+tot = sum(buf[i] for i in range(7))
+print("encode %.2f ms, %d tiles, %.0f cycles/tile total (memtime units)" % (dt * 1e3, tiles, tot / tiles))
+for i, n in enumerate(names):
+  print("  %-22s %8.0f  %5.1f%%" % (n, buf[i] / tiles, 100.0 * buf[i] / tot))
