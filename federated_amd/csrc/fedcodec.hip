@@ -21,6 +21,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <algorithm>
+#include <cmath>
 #include <string>
 
 #include "../../include/fedcodec.h"
@@ -80,11 +81,12 @@ __device__ __forceinline__ int32_t f2i_x86(float r) {
 }
 
 // quantize_utils.py:33-36 / 46-53 / 62-66 for one element.  Returns q and the
-// client-side dequantised value (quantize_encode.py:148-149).
-template <int MODE>
-__device__ __forceinline__ int32_t quantize_one(float x, float step, uint32_t rbits,
+// client-side dequantised value (quantize_encode.py:148-149).  RCP: step is a
+// power of two, so x / step == x * (1 / step) exactly (FTZ included).
+template <int MODE, bool RCP = false>
+__device__ __forceinline__ int32_t quantize_one(float x, float step, float rcp, uint32_t rbits,
                                                 float& deq, float& noise) {
-  const float sc = x / step;  // IEEE-correct division, FTZ/DAZ
+  const float sc = RCP ? x * rcp : x / step;  // IEEE-correct division, FTZ/DAZ
   float r;
   noise = 0.0f;
   if (MODE == FC_UNIFORM) {
@@ -210,6 +212,7 @@ struct EncodeArgs {
   int64_t P;
   int32_t T;  // tiles per client
   float step;
+  float rcp;  // 1 / step when step is a power of two (exact reciprocal path)
   const float* norms;
   const int64_t* seeds;
   uint8_t* stream_buf;
@@ -235,6 +238,7 @@ struct EncShared {
   uint32_t tail;
   uint32_t ticket;
   uint32_t next_ticket;
+  uint32_t slow;  // tile needs the slow (re-quantise) emission path
   // look-back results broadcast to the workgroup
   uint64_t b0;
   int32_t last_before;
@@ -406,6 +410,7 @@ __device__ __forceinline__ void load_raw(const EncodeArgs& a, uint32_t ticket, i
 
 struct ClientQ {
   float step;
+  float rcp;
   Key4 key;
 };
 
@@ -414,13 +419,14 @@ __device__ __forceinline__ ClientQ client_q(const EncodeArgs& a, int32_t c) {
   ClientQ r;
   r.step = a.step;
   if (!INT_IN && a.norms) r.step = a.norms[c] * a.step;
+  r.rcp = a.rcp;
   r.key = Key4{0, 0, 0, 0};
   if (!INT_IN && MODE != FC_UNIFORM) r.key = tf_seed_scramble(a.seeds[2 * c], a.seeds[2 * c + 1]);
   return r;
 }
 
 // Quantise one chunk of 4 consecutive elements starting at e0.
-template <int MODE, bool INT_IN>
+template <int MODE, bool INT_IN, bool RCP>
 __device__ __forceinline__ void quant_chunk(const ClientQ& cq, int64_t e0, int64_t P,
                                             const uint32_t (&r4)[4], int32_t (&q4)[4],
                                             float& dist) {
@@ -435,26 +441,96 @@ __device__ __forceinline__ void quant_chunk(const ClientQ& cq, int64_t e0, int64
     for (int k = 0; k < 4; ++k) {
       float deq, noise;
       const float xv = __uint_as_float(r4[k]);
-      const int32_t qq = quantize_one<MODE>(xv, cq.step, rr[k], deq, noise);
+      const int32_t qq = quantize_one<MODE, RCP>(xv, cq.step, cq.rcp, rr[k], deq, noise);
       const bool valid = e0 + k < P;
       q4[k] = valid ? qq : 0;
       const float dd = xv - deq;
-      dist += valid ? dd * dd : 0.0f;
+      dist = valid ? fmaf(dd, dd, dist) : dist;
     }
   }
 }
 
-template <int MODE, bool INT_IN>
-__device__ __forceinline__ void quantize_raw(const EncodeArgs& a, int32_t c, int64_t tile_base,
-                                             int wv, int lane, const uint32_t (&raw)[4][4],
-                                             int32_t (&q)[4][4], float& dist) {
+// Run-length gamma code of one chunk of 4 consecutive elements (branch-free),
+// built right after the chunk is quantised so the int32 values never stay live:
+// acc holds the concatenated codes after the chunk's first nonzero's run code
+// (that one depends on the previous chunks and is prepended in phase C).
+struct ChunkCode {
+  uint64_t acc;
+  uint32_t len;
+  uint32_t lng;   // a code > 32 bits or more than 64 bits in the chunk
+  int32_t first;  // tile-relative first nonzero of the chunk, or -1
+  int32_t last;   // tile-relative last nonzero of the chunk, or -1
+};
+
+__device__ __forceinline__ ChunkCode chunk_local(const int32_t (&q4)[4], int32_t rel0) {
+  ChunkCode r;
+  r.acc = 0;
+  r.len = 0;
+  r.lng = 0;
+  r.first = -1;
+  int32_t pk = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int32_t v = q4[k];
+    const bool nz = v != 0;
+    const uint32_t m = mag_u32(v);
+    const uint32_t ml = 2u * (31u - __clz(m | 1u)) + 1u;
+    const uint32_t d = (uint32_t)(k - pk);
+    const uint32_t rl = pk >= 0 ? 2u * (31u - __clz(d)) + 1u : 0u;
+    const uint32_t L = rl + 1u + ml;
+    const uint32_t code = ((pk >= 0 && L <= 32u) ? (d << (1u + ml)) : 0u) | ((uint32_t)(v > 0) << ml) | m;
+    r.lng |= (nz && L > 32u) ? 1u : 0u;
+    r.acc = nz ? (r.acc << L) | code : r.acc;
+    r.len += nz ? L : 0u;
+    r.first = (r.first < 0 && nz) ? rel0 + k : r.first;
+    pk = nz ? k : pk;
+  }
+  r.last = pk >= 0 ? rel0 + pk : -1;
+  r.lng |= r.len > 64u ? 1u : 0u;
+  return r;
+}
+
+// Prepend the run code of the chunk's first nonzero once the last nonzero
+// before the chunk (prev, tile-relative, -1 = none in this tile) is known.
+__device__ __forceinline__ void chunk_prepend(ChunkCode& r, int32_t prev) {
+  if (r.first >= 0 && prev >= 0) {
+    const uint32_t d = (uint32_t)(r.first - prev);
+    const uint32_t rl = 2u * (31u - __clz(d)) + 1u;
+    r.lng |= (r.len + rl > 64u) ? 1u : 0u;
+    r.acc = (r.len + rl > 64u) ? 0 : (((uint64_t)d << r.len) | r.acc);
+    r.len += rl;
+  }
+}
+
+template <int MODE, bool INT_IN, bool RCP>
+__device__ __forceinline__ void quantize_tile(const EncodeArgs& a, int32_t c, int64_t tile_base,
+                                              int wv, int lane, const uint32_t (&raw)[4][4],
+                                              ChunkCode (&cc)[4], float& dist, int32_t& nnz) {
   const ClientQ cq = client_q<MODE, INT_IN>(a, c);
   dist = 0.0f;
+  nnz = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int64_t e0 = tile_base + 1024 * wv + 256 * j + 4 * lane;
-    quant_chunk<MODE, INT_IN>(cq, e0, a.P, raw[j], q[j], dist);
+    const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
+    int32_t q4[4];
+    quant_chunk<MODE, INT_IN, RCP>(cq, tile_base + rel0, a.P, raw[j], q4, dist);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
+    cc[j] = chunk_local(q4, rel0);
   }
+}
+
+// Re-read and re-quantise one chunk (slow path: tiles with codes > 32 bits or
+// a body larger than the LDS window).
+template <int MODE, bool INT_IN, bool RCP>
+__device__ __forceinline__ void reload_chunk(const EncodeArgs& a, const ClientQ& cq, int32_t c,
+                                             int64_t e0, int32_t (&q4)[4]) {
+  const uint32_t* xp = (const uint32_t*)a.xs[c];
+  uint32_t r4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r4[k] = (e0 + k < a.P) ? xp[e0 + k] : 0u;
+  float dd = 0.0f;
+  quant_chunk<MODE, INT_IN, RCP>(cq, e0, a.P, r4, q4, dd);
 }
 
 #ifdef FC_STAMPS
@@ -471,7 +547,7 @@ __device__ unsigned long long g_stamps[8];
 #define STAMP(i) do {} while (0)
 #endif
 
-template <int MODE, bool INT_IN>
+template <int MODE, bool INT_IN, bool RCP>
 __global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
   __shared__ EncShared sh;
   const int tid = threadIdx.x;
@@ -495,6 +571,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
     if (tid == 0) {
       sh.next_ticket = atomicAdd(a.counter, 1u);  // read after the first barrier
       sh.tail = 0;
+      sh.slow = 0;
     }
     // tickets interleave clients (tile-major) so each client has few tiles in
     // flight and the look-back almost always finds a prefix at distance 1
@@ -504,28 +581,20 @@ __global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
     const int64_t tile_base = (int64_t)t * kTE;
     const bool last_tile = (t == a.T - 1);
 
-    // ---- phase A: quantise (thread owns 4 chunks of 4 consecutive elements) ----
-    int32_t q[4][4];
+    // ---- phase A: quantise + chunk-local codes (4 chunks of 4 consecutive elements) ----
+    ChunkCode cc[4];
     float dist;
-    quantize_raw<MODE, INT_IN>(a, c, tile_base, wv, lane, raw, q, dist);
+    int32_t nnz;
+    quantize_tile<MODE, INT_IN, RCP>(a, c, tile_base, wv, lane, raw, cc, dist, nnz);
     STAMP(1);
 
-    // ---- phase B: max-scan of nonzero positions (tile-relative) ----
-    int32_t chunk_prev[4];  // last nonzero before the chunk, or -1
-    int32_t carry = -1, wfirst = 0x7FFFFFFF, nnz = 0;
+    // ---- phase B: wave max-scan of the chunks' last nonzero ----
+    int32_t chunk_prev[4];  // last nonzero before the chunk (tile-relative), or -1
+    int32_t carry = -1, wfirst = 0x7FFFFFFF;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-      int32_t cl = -1;
-#pragma unroll
-      for (int k = 3; k >= 0; --k) {
-        nnz += q[j][k] != 0;
-        if (q[j][k] != 0) wfirst = min(wfirst, rel0 + k);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (q[j][k] != 0) cl = rel0 + k;
-      const int32_t incl = dpp_incl_max(cl);
+      wfirst = min(wfirst, cc[j].first >= 0 ? cc[j].first : 0x7FFFFFFF);
+      const int32_t incl = dpp_incl_max(cc[j].last);
       chunk_prev[j] = max(dpp_shr1(incl, -1), carry);
       carry = max(carry, lane63(incl));
     }
@@ -564,29 +633,23 @@ __global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
     }
     const uint32_t next = sh.next_ticket;
 
-    // ---- phase C: body code lengths, sum-scan ----
-    uint32_t chunk_off[4];
-    uint32_t wbits = 0;
+    // ---- phase C: complete the chunk codes, sum-scan of their lengths ----
+    uint64_t cacc[4];
+    uint32_t chunk_off[4], clen[4];
+    uint32_t wbits = 0, lng = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       chunk_prev[j] = max(chunk_prev[j], wave_in);
-      const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-      int32_t prev = chunk_prev[j];
-      uint32_t bits = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int32_t v = q[j][k];
-        if (v != 0) {
-          const uint32_t rl = prev >= 0 ? glen((uint32_t)(rel0 + k - prev)) : 0u;
-          bits += rl + 1u + glen(mag_u32(v));
-          prev = rel0 + k;
-        }
-      }
-      const uint32_t incl = dpp_incl_sum(bits);
-      chunk_off[j] = wbits + incl - bits;
+      chunk_prepend(cc[j], chunk_prev[j]);
+      cacc[j] = cc[j].acc;
+      clen[j] = cc[j].len;
+      lng |= cc[j].lng;
+      const uint32_t incl = dpp_incl_sum(cc[j].len);
+      chunk_off[j] = wbits + incl - cc[j].len;
       wbits += (uint32_t)lane63((int32_t)incl);
     }
     if (lane == 0) sh.wave_bits[wv] = wbits;
+    if (lng) sh.slow = 1;
     __syncthreads();
     STAMP(3);
     uint32_t woff = 0, body = 0;
@@ -595,69 +658,47 @@ __global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
       woff += (w < wv) ? sh.wave_bits[w] : 0u;
       body += sh.wave_bits[w];
     }
-    // fast path: the whole body (+ trailing code + one funnel word) fits the window
-    const bool fast = body + 64u <= 32u * (kWinWords - 1);
+    // fast path: no code > 32 bits and the body (+ trailing code + one funnel
+    // word) fits the LDS window
+    const bool fast = !sh.slow && body + 64u <= 32u * (kWinWords - 1);
 
-    // ---- phase D: emit the body at body-relative bit offsets (fast path) or
-    //      just its last 32 bits (slow path); then prefetch the next tile ----
+    // ---- phase D: emit the body at body-relative bit offsets (fast path), or
+    //      compute just its last 32 bits (slow path); prefetch the next tile ----
+    if (fast) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t off = woff + chunk_off[j];
-      if (!fast && off + 4 * 89 + 32 < body) continue;
-      const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-      int32_t prev = chunk_prev[j];
-      uint32_t pos = off;
-      uint64_t acc = 0;  // pending bits of this chunk (fast path)
-      uint32_t nacc = 0, accpos = off;
+      for (int j = 0; j < 4; ++j)
+        if (clen[j]) win_emit(sh.win, cacc[j], clen[j], woff + chunk_off[j], 0);
+    } else {
+      // slow tile: recompute codes element by element (any length) for the tail
+      const ClientQ cq = client_q<MODE, INT_IN>(a, c);
+#pragma unroll 1
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t off = woff + (j == 0 ? chunk_off[0] : j == 1 ? chunk_off[1] : j == 2 ? chunk_off[2] : chunk_off[3]);
+        const uint32_t cl = (j == 0 ? clen[0] : j == 1 ? clen[1] : j == 2 ? clen[2] : clen[3]);
+        if (off + cl + 32 < body || cl == 0) continue;
+        const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
+        int32_t qv[4];
+        reload_chunk<MODE, INT_IN, RCP>(a, cq, c, tile_base + rel0, qv);
+        int32_t prev = (j == 0 ? chunk_prev[0] : j == 1 ? chunk_prev[1] : j == 2 ? chunk_prev[2] : chunk_prev[3]);
+        uint32_t pos = off;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int32_t v = q[j][k];
-        if (v == 0) continue;
-        const uint32_t m = mag_u32(v);
-        const uint32_t ml = glen(m);
-        const uint64_t sm = ((uint64_t)(v > 0) << ml) | m;
-        uint64_t code;
-        uint32_t L;
-        if (prev >= 0) {
-          const uint32_t d = (uint32_t)(rel0 + k - prev);
-          const uint32_t rl = glen(d);
-          L = rl + 1 + ml;
-          if (L <= 64) {
-            code = ((uint64_t)d << (1 + ml)) | sm;
-          } else {  // rare: > 64-bit code, emit the run code on its own
-            if (fast) {
-              if (nacc) win_emit(sh.win, acc, nacc, accpos, 0);
-              win_emit(sh.win, d, rl, pos, 0);
-              acc = 0;
-              nacc = 0;
-            } else {
-              tail_emit(&sh.tail, d, rl, pos + rl, body);
-            }
+        for (int k = 0; k < 4; ++k) {
+          const int32_t v = qv[k];
+          if (v == 0) continue;
+          if (prev >= 0) {
+            const uint32_t d = (uint32_t)(rel0 + k - prev);
+            const uint32_t rl = glen(d);
             pos += rl;
-            accpos = pos;
-            code = sm;
-            L = 1 + ml;
+            tail_emit(&sh.tail, d, rl, pos, body);
           }
-        } else {
-          code = sm;
-          L = 1 + ml;
+          const uint32_t m = mag_u32(v);
+          const uint32_t ml = glen(m);
+          const uint64_t sm = ((uint64_t)(v > 0) << ml) | m;
+          pos += 1 + ml;
+          tail_emit(&sh.tail, sm, 1 + ml, pos, body);
+          prev = rel0 + k;
         }
-        if (fast) {
-          if (nacc + L > 64) {
-            win_emit(sh.win, acc, nacc, accpos, 0);
-            acc = 0;
-            nacc = 0;
-            accpos = pos;
-          }
-          acc = (L >= 64 ? 0 : acc << L) | code;
-          nacc += L;
-        } else {
-          tail_emit(&sh.tail, code, L, pos + L, body);
-        }
-        pos += L;
-        prev = rel0 + k;
       }
-      if (fast && nacc) win_emit(sh.win, acc, nacc, accpos, 0);
     }
     if (next < total_tiles) load_raw<INT_IN>(a, next, wv, lane, raw);
     __syncthreads();
@@ -764,10 +805,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
       const uint32_t nt = min((uint32_t)kWinWords, (body + sh.trail_len + 31) / 32 + 1);
       for (uint32_t i = tid; i < nt; i += kThreads) sh.win[i] = 0;
     } else {
-      // slow path (codes > 16 bits/element on average): re-read and re-quantise
-      // this tile one chunk at a time and emit stream-relative in window passes
+      // slow path (a code > 32 bits, or a body larger than the LDS window):
+      // re-read and re-quantise this tile one chunk at a time and emit
+      // stream-relative in window passes
       const ClientQ cq = client_q<MODE, INT_IN>(a, c);
-      const uint32_t* xp = (const uint32_t*)a.xs[c];
       const uint32_t npass = (nwords_owned + kWinWords - 1) / kWinWords;
       for (uint32_t pass = 0; pass < npass; ++pass) {
         const uint32_t plo = pass * kWinWords;
@@ -782,16 +823,11 @@ __global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
 #pragma unroll 1
         for (int j = 0; j < 4; ++j) {
           const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-          const int64_t e0 = tile_base + rel0;
           int32_t prev = j == 0 ? chunk_prev[0] : j == 1 ? chunk_prev[1] : j == 2 ? chunk_prev[2] : chunk_prev[3];
           uint32_t pos = bstart + woff +
                          (j == 0 ? chunk_off[0] : j == 1 ? chunk_off[1] : j == 2 ? chunk_off[2] : chunk_off[3]);
-          uint32_t r4[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) r4[k] = (e0 + k < P) ? xp[e0 + k] : 0u;
           int32_t q4[4];
-          float dd = 0.0f;
-          quant_chunk<MODE, INT_IN>(cq, e0, P, r4, q4, dd);
+          reload_chunk<MODE, INT_IN, RCP>(a, cq, c, tile_base + rel0, q4);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const int32_t v = q4[k];
@@ -1010,7 +1046,7 @@ __global__ void k_quantize(const float* __restrict__ x, int64_t P, float step, K
   for (int k = 0; k < 4; ++k) {
     if (e0 + k < P) {
       float deq, nz;
-      q[e0 + k] = quantize_one<MODE>(x[e0 + k], step, rr[k], deq, nz);
+      q[e0 + k] = quantize_one<MODE>(x[e0 + k], step, 0.0f, rr[k], deq, nz);
       if (noise) noise[e0 + k] = (MODE == FC_UNIFORM) ? 0.0f : (MODE == FC_DITHERED ? nz : u01(rr[k]) - 0.5f);
     }
   }
@@ -1248,14 +1284,22 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   int64_t max_grid = std::min<int64_t>((int64_t)ncu * 8, std::max<int64_t>(128, 64LL * nclients));
   if (const char* g = getenv("FEDCODEC_ENC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
   const int grid = (int)std::min<int64_t>(total, max_grid);
+  // power-of-two step (no per-client normalisation): x / step == x * (1 / step)
+  int ex = 0;
+  const bool pow2 = !int_in && !norms && std::frexp(step, &ex) == 0.5f && std::isnormal(1.0f / step);
+  a.rcp = pow2 ? 1.0f / step : 0.0f;
+  const dim3 g(grid), b(kThreads);
   if (int_in) {
-    hipLaunchKernelGGL((k_encode<FC_UNIFORM, true>), dim3(grid), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((k_encode<FC_UNIFORM, true, false>), g, b, 0, s, a);
   } else if (mode == FC_UNIFORM) {
-    hipLaunchKernelGGL((k_encode<FC_UNIFORM, false>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (pow2) hipLaunchKernelGGL((k_encode<FC_UNIFORM, false, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_encode<FC_UNIFORM, false, false>), g, b, 0, s, a);
   } else if (mode == FC_STOCHASTIC) {
-    hipLaunchKernelGGL((k_encode<FC_STOCHASTIC, false>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (pow2) hipLaunchKernelGGL((k_encode<FC_STOCHASTIC, false, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_encode<FC_STOCHASTIC, false, false>), g, b, 0, s, a);
   } else {
-    hipLaunchKernelGGL((k_encode<FC_DITHERED, false>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (pow2) hipLaunchKernelGGL((k_encode<FC_DITHERED, false, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_encode<FC_DITHERED, false, false>), g, b, 0, s, a);
   }
   return check_launch("k_encode");
 }

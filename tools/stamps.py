@@ -16,7 +16,9 @@ P = int(os.environ.get("P", 25_000_000))
 C = int(os.environ.get("C", 128))
 mode = int(os.environ.get("MODE", _lib.STOCHASTIC))
 lib = _lib.load()
-lib.fc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+HAVE = hasattr(lib, "fc_debug_stamps")
+if HAVE:
+  lib.fc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev)
 g.manual_seed(1)
@@ -27,14 +29,19 @@ seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
 batch = codec.EncodedBatch(P, C, [P + 1024] * C, dev)
 buf = (ctypes.c_ulonglong * 8)()
 for it in range(3):
-  lib.fc_debug_stamps(buf, 1)
+  if HAVE:
+    lib.fc_debug_stamps(buf, 1)
   torch.cuda.synchronize()
   t0 = time.perf_counter()
   codec.quantize_encode(None, 0.5, seeds, mode, ptrs=ptrs, P=P, out=batch)
   torch.cuda.synchronize()
   dt = time.perf_counter() - t0
-  lib.fc_debug_stamps(buf, 0)
+  if HAVE:
+    lib.fc_debug_stamps(buf, 0)
 tiles = C * codec.num_tiles(P)
+if not HAVE:
+  print("encode %.2f ms (no stamps in this build)" % (dt * 1e3))
+  sys.exit(0)
 names = ["ticket+barrier", "A load+quantize", "B maxscan+barrier", "C lengths+barrier",
          "D tail+barrier", "E lookback+barrier", "F emit+store"]
 tot = sum(buf[i] for i in range(7))
