@@ -887,54 +887,49 @@ struct DecodeArgs {
   int32_t* err;
 };
 
+// MSB-first bit reader over one client's code: a 64-bit window plus one
+// prefetched 32-bit word, so each refill's load is issued ~one refill early.
 struct BitReader {
   const uint4* p;    // next 16-byte block to fetch
   const uint4* end;  // first block beyond the client's region
-  uint4 nxt;         // prefetched block
-  uint32_t blk[4];   // current block
-  int bi;            // next word index in blk
+  uint4 nxt;         // prefetched raw block, consumed one reservoir later
+  uint32_t nxtok;    // nxt lies inside the region
+  uint64_t rhi, rlo; // reservoir: next 128 bits after the window, MSB aligned
+  int rbits;         // valid bits in the reservoir (multiple of 32)
   uint64_t win;      // next bits, MSB aligned
-  int nwin;          // valid bits in win
+  int nwin;          // valid bits in win (>= 32 after refill)
 
-  __device__ __forceinline__ uint4 fetch() {
-    uint4 r = make_uint4(0, 0, 0, 0);
-    if (p < end) r = *p;
+  __device__ __forceinline__ void prefetch() {
+    nxtok = p < end;
+    nxt = *(nxtok ? p : end - 1);  // unconditional 16-byte load: no branch, no early wait
     ++p;
-    return r;
   }
-  __device__ __forceinline__ void init(const uint8_t* base, int64_t cap, uint64_t bit) {
-    const uint64_t blk_i = bit >> 7;
-    p = (const uint4*)base + blk_i;
-    end = (const uint4*)base + (cap >> 4);
-    const uint4 b = fetch();
-    nxt = fetch();
-    blk[0] = bswap32(b.x); blk[1] = bswap32(b.y); blk[2] = bswap32(b.z); blk[3] = bswap32(b.w);
-    const int wi = (int)((bit >> 5) & 3);
-    bi = wi;
-    win = 0;
-    nwin = 0;
-    refill();
-    refill();
-    const int skip = (int)(bit & 31);
-    win <<= skip;
-    nwin -= skip;
+  __device__ __forceinline__ void load_reservoir() {
+    const uint4 b = nxtok ? nxt : make_uint4(0, 0, 0, 0);
+    rhi = ((uint64_t)bswap32(b.x) << 32) | bswap32(b.y);
+    rlo = ((uint64_t)bswap32(b.z) << 32) | bswap32(b.w);
+    rbits = 128;
+    prefetch();
   }
   __device__ __forceinline__ uint32_t next_word() {
-    if (bi == 4) {
-      const uint4 b = nxt;
-      nxt = fetch();
-      blk[0] = bswap32(b.x); blk[1] = bswap32(b.y); blk[2] = bswap32(b.z); blk[3] = bswap32(b.w);
-      bi = 0;
-    }
-    uint32_t w;
-    switch (bi) {
-      case 0: w = blk[0]; break;
-      case 1: w = blk[1]; break;
-      case 2: w = blk[2]; break;
-      default: w = blk[3]; break;
-    }
-    ++bi;
+    if (rbits == 0) load_reservoir();
+    const uint32_t w = (uint32_t)(rhi >> 32);
+    rhi = (rhi << 32) | (rlo >> 32);
+    rlo <<= 32;
+    rbits -= 32;
     return w;
+  }
+  __device__ __forceinline__ void init(const uint8_t* base, int64_t cap, uint64_t bit) {
+    p = (const uint4*)base + (bit >> 7);
+    end = (const uint4*)base + (cap >> 4);
+    prefetch();
+    load_reservoir();
+    for (int i = (int)((bit >> 5) & 3); i > 0; --i) (void)next_word();
+    win = ((uint64_t)next_word() << 32);
+    win |= next_word();
+    const int skip = (int)(bit & 31);
+    win <<= skip;
+    nwin = 64 - skip;
   }
   __device__ __forceinline__ void refill() {
     if (nwin <= 32) {
@@ -945,38 +940,64 @@ struct BitReader {
   // Consume n <= 32 bits (caller guarantees nwin >= n).
   __device__ __forceinline__ uint32_t take(int n) {
     const uint32_t v = (uint32_t)(win >> (64 - n));
-    win <<= n;
+    win = n >= 64 ? 0 : win << n;
     nwin -= n;
     refill();
     return v;
   }
-  // Gamma-coded value (1 .. 2^32-1).  Returns 0 on a malformed code.
+  // Gamma-coded value (1 .. 2^32-1), general path.  Returns 0 on a malformed code.
   __device__ __forceinline__ uint32_t gamma() {
-    int z = win ? __clzll(win) : 64;
-    if (z > nwin) z = nwin;
-    if (2 * z + 1 <= nwin) {
-      const int L = 2 * z + 1;
-      const uint32_t v = (uint32_t)(win >> (64 - L));
-      win <<= L;
-      nwin -= L;
-      refill();
-      return v;
-    }
-    // long code: consume the zeros first (at most 31 of them)
     int zeros = 0;
     for (;;) {
-      int zz = win ? __clzll(win) : 64;
-      if (zz > nwin) zz = nwin;
+      int zz = win ? (int)__clzll(win) : 64;
+      if (zz >= nwin) {  // the whole window is zeros
+        zeros += nwin;
+        win = 0;
+        nwin = 0;
+        refill();
+        if (zeros > 31) return 0;
+        continue;
+      }
       zeros += zz;
-      win = zz >= 64 ? 0 : win << zz;
+      win <<= zz;
       nwin -= zz;
       refill();
-      if (zz < 32 || zeros > 31) break;
+      break;
     }
     if (zeros > 31) return 0;
     return take(zeros + 1);
   }
 };
+
+__device__ __forceinline__ uint64_t shl64(uint64_t x, uint32_t n) { return n >= 64 ? 0 : x << n; }
+
+// One nonzero's code: run gamma d, sign bit, magnitude gamma m.  Returns the
+// bits consumed (0 on a malformed code).
+__device__ __forceinline__ uint32_t decode_code(BitReader& br, uint32_t& d, int32_t& val) {
+  const uint64_t w = br.win;
+  const uint32_t z1 = w ? (uint32_t)__clzll(w) : 64u;
+  const uint32_t L1 = 2u * z1 + 1u;
+  const uint64_t w3 = shl64(w, L1 + 1u);
+  const uint32_t z2 = w3 ? (uint32_t)__clzll(w3) : 64u;
+  const uint32_t L2 = 2u * z2 + 1u;
+  const uint32_t L = L1 + 1u + L2;
+  if (L <= (uint32_t)br.nwin && L1 <= 32u && L2 <= 32u) {  // fast path: whole code in the window
+    d = (uint32_t)(w >> (64u - L1));
+    const uint32_t s = (uint32_t)(shl64(w, L1) >> 63);
+    const uint32_t m = (uint32_t)(w3 >> (64u - L2));
+    val = (int32_t)(s ? m : 0u - m);
+    br.win = shl64(w3, L2);
+    br.nwin -= (int)L;
+    br.refill();
+    return L;
+  }
+  d = br.gamma();
+  const uint32_t s = br.take(1);
+  const uint32_t m = br.gamma();
+  val = (int32_t)(s ? m : 0u - m);
+  if (d == 0 || m == 0) return 0;
+  return 2u * (31u - __clz(d)) + 1u + 1u + 2u * (31u - __clz(m)) + 1u;
+}
 
 __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
   extern __shared__ int32_t acc[];  // [tiles_per_wg][kTE]
@@ -996,22 +1017,21 @@ __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
       const uint64_t e0 = a.idx[ib], e1 = a.idx[ib + 1];
       const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
       if (bend <= bstart) continue;
-      int64_t pos = (int64_t)(e0 >> 36) - 1;  // last nonzero before the tile
+      int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
       BitReader br;
       br.init(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart);
-      uint64_t consumed = bstart;
-      while (consumed < bend) {
-        const uint32_t d = br.gamma();
-        const uint32_t s = br.take(1);
-        const uint32_t m = br.gamma();
-        consumed += 2 * (31 - __clz(d | 1)) + 1 + 1 + 2 * (31 - __clz(m | 1)) + 1;
-        pos += d;
-        const int64_t rel = pos - tile_base;
-        if (d == 0 || m == 0 || rel < 0 || rel >= kTE) {
+      int64_t rem = (int64_t)(bend - bstart);
+      while (rem > 0) {
+        uint32_t d;
+        int32_t v;
+        const uint32_t L = decode_code(br, d, v);
+        rel += (int32_t)d;
+        if (L == 0 || (uint32_t)rel >= (uint32_t)kTE) {
           atomicOr(a.err, 1);
           break;
         }
-        atomicAdd(&my[rel], (int32_t)(s ? m : 0u - m));
+        atomicAdd(&my[rel], v);
+        rem -= L;
       }
     }
   }
