@@ -10,7 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDCODEC_LIB") or os.path.join(_HERE, "libfedcodec.so")
 
 UNIFORM, STOCHASTIC, DITHERED = 0, 1, 2
-NORM_MEAN_MAGNITUDE, NORM_MAX_MAGNITUDE, NORM_DIMENSIONLESS = 1, 2, 3
+NORM_MEAN_MAGNITUDE, NORM_MAX_MAGNITUDE, NORM_DIMENSIONLESS, NORM_L2, NORM_LINF = 1, 2, 3, 4, 5
 TILE_ELEMS = 4096
 MAX_ELEMS = (1 << 26) - 1
 
@@ -26,8 +26,8 @@ SIGNATURES = {
     "fc_num_tiles": (_I64, [_I64]),
     "fc_encode_workspace_bytes": (_I64, [_I32, _I64]),
     "fc_quantize": (_INT, [_P, _I64, _F32, _I64, _I64, _INT, _P, _P, _P]),
-    "fc_quantize_encode": (_INT, [_P, _I32, _I64, _F32, _P, _P, _INT, _P, _P, _P, _P, _P, _P,
-                                  _P, _P, _P, _I64, _P]),
+    "fc_quantize_encode": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P,
+                                  _P, _P, _P, _P, _I64, _P]),
     "fc_rlgamma_encode": (_INT, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "fc_decode_accumulate": (_INT, [_P, _P, _P, _P, _I32, _I64, _P, _P, _P, _F32, _P, _P, _P]),
     "fc_dequantize": (_INT, [_P, _I64, _F32, _P, _P, _P]),

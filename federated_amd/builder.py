@@ -1,0 +1,202 @@
+"""Aggregator-factory surface of compressed_communication/builder.py, MI355X-backed.
+
+``build_quantization_encode_aggregator`` is the drop-in point
+(builder.py:453-525): same name, keyword arguments, defaults and ValueError
+messages.  It wraps ``QuantizeEncodeFactory`` with ``configure_aggregator``
+(builder.py:37-119) in the reference order: concat -> (weighted) mean ->
+adaptive clipping -> adaptive zeroing.  TFF is not installed here, so those TFF
+wrappers are restated (``WrappedAggregationFactory`` below):
+
+* concat_factory: each client's list of tensors is flattened and concatenated
+  (on device);
+* MeanFactory (builder.py:100-101): value * weight, inner sum, / sum(weight)
+  (divide_no_nan); UnweightedMeanFactory: / number of clients;
+* clipping_factory with ``PrivateQuantileEstimationProcess.no_noise(
+  initial_estimate=1.0, target_quantile=0.8, learning_rate=0.2)``
+  (builder.py:104-109): scale = C * min(1 / ||x||_2, 1 / C) as
+  ``tf.clip_by_global_norm``, geometric update C <- C * exp(-lr * (frac(||x||
+  <= C) - q));
+* zeroing_factory with ``no_noise(10.0, 0.98, log(10), multiplier=2,
+  increment=1)`` (builder.py:110-117): a client whose max |x| exceeds
+  2 * X + 1 is zeroed; same geometric update on X.
+
+The clip scale and the client weight are fused into the HIP encoder as a
+per-client pre-scale (``fc_quantize_encode`` prescale), so they cost no extra
+HBM pass.  Parity of the wrappers with TFF is **unpinned** (TFF absent; no
+fixture in the reference holds their outputs).
+"""
+import collections
+import math
+
+import numpy as np
+import torch
+
+from federated_amd import _lib
+from federated_amd import codec
+from federated_amd import tff_compat as tc
+from federated_amd.aggregators import quantize_encode
+
+F32 = np.float32
+
+
+class QuantileEstimate:
+  """``PrivateQuantileEstimationProcess.no_noise`` (geometric update) restated."""
+
+  def __init__(self, initial_estimate, target_quantile, learning_rate, multiplier=1.0,
+               increment=0.0):
+    self.initial_estimate = F32(initial_estimate)
+    self.target_quantile = F32(target_quantile)
+    self.learning_rate = F32(learning_rate)
+    self.multiplier = F32(multiplier)
+    self.increment = F32(increment)
+
+  def report(self, estimate):
+    return F32(estimate * self.multiplier + self.increment)
+
+  def update(self, estimate, norms):
+    thr = self.report(estimate)
+    below = F32(np.mean((np.asarray(norms, np.float32) <= thr).astype(np.float32)))
+    return F32(estimate * np.exp(-self.learning_rate * (below - self.target_quantile)))
+
+
+class WrappedAggregationFactory(tc.WeightedAggregationFactory):
+  """concat -> mean -> clipping -> zeroing around an inner codec factory."""
+
+  def __init__(self, inner, concatenate=True, weighted=True, clipping=True, zeroing=True):
+    self._inner = inner
+    self._concatenate = concatenate
+    self._weighted = weighted
+    self._clip = QuantileEstimate(1.0, 0.8, 0.2) if clipping else None
+    self._zero = (QuantileEstimate(10.0, 0.98, math.log(10.0), multiplier=2.0, increment=1.0)
+                  if zeroing else None)
+
+  def create(self, value_type, weight_type=None):
+    value_type = tc.to_type(value_type)
+    parts = list(value_type) if isinstance(value_type, tc.StructType) else [value_type]
+    if not self._concatenate and len(parts) != 1:
+      raise NotImplementedError("concatenate=False over a structure is not supported")
+    P = int(sum(t.num_elements for t in parts))
+    inner = self._inner.create(tc.TensorType(np.float32, (P,)))
+    wrap = self
+
+    def init_fn():
+      return collections.OrderedDict(
+          zeroing_norm=wrap._zero.initial_estimate if wrap._zero else (),
+          clipping_norm=wrap._clip.initial_estimate if wrap._clip else (),
+          inner_state=inner.initialize())
+
+    def flat(v):
+      seq = v if isinstance(v, (list, tuple)) and len(parts) > 1 else [v]
+      ts = [torch.as_tensor(np.asarray(x, np.float32) if not isinstance(x, torch.Tensor) else x)
+            .cuda().reshape(-1).to(torch.float32) for x in seq]
+      return torch.cat(ts) if len(ts) > 1 else ts[0].contiguous()
+
+    def unflat(t):
+      out, off = [], 0
+      for ty in parts:
+        n = ty.num_elements
+        out.append(t[off:off + n].reshape(ty.shape).cpu().numpy())
+        off += n
+      return out if len(parts) > 1 else out[0]
+
+    def next_fn(state, value, weight=None, seeds=None):
+      rows = [flat(v) for v in value]
+      C = len(rows)
+      w = (np.asarray(weight, np.float32).reshape(C) if (wrap._weighted and weight is not None)
+           else np.ones(C, np.float32))
+      s0 = np.ones(C, np.float32)
+      zero_norm = clip_norm = ()
+      if wrap._zero:
+        linf = codec.client_norms(rows, _lib.NORM_LINF).cpu().numpy()
+        zero_norm = wrap._zero.report(state["zeroing_norm"])
+        keep = ~(linf > zero_norm)
+        s0 = np.where(keep, s0, F32(0.0)).astype(np.float32)
+      if wrap._clip:
+        l2 = codec.client_norms(rows, _lib.NORM_L2).cpu().numpy()
+        l2 = np.where(s0 == 0, F32(0.0), l2).astype(np.float32)  # zeroed clients have norm 0
+        clip_norm = wrap._clip.report(state["clipping_norm"])
+        with np.errstate(divide="ignore"):
+          inv = np.where(l2 > 0, F32(1.0) / l2, np.float32(np.inf)).astype(np.float32)
+        scale = (clip_norm * np.minimum(inv, F32(1.0) / clip_norm)).astype(np.float32)
+        s0 = (s0 * scale).astype(np.float32)
+      prescale = np.stack([s0, w], axis=1)
+      out = inner.next(state["inner_state"], rows, seeds=seeds, prescale=prescale)
+      denom = F32(np.sum(w, dtype=np.float32)) if wrap._weighted else F32(C)
+      res = torch.as_tensor(out.result).cuda().reshape(-1)
+      res = res / denom if denom != 0 else torch.zeros_like(res)
+      new_state = collections.OrderedDict(
+          zeroing_norm=(wrap._zero.update(state["zeroing_norm"], linf) if wrap._zero else ()),
+          clipping_norm=(wrap._clip.update(state["clipping_norm"], l2) if wrap._clip else ()),
+          inner_state=out.state)
+      measurements = collections.OrderedDict(
+          zeroing_norm=zero_norm, clipping_norm=clip_norm,
+          mean_value=out.measurements)
+      return tc.MeasuredProcessOutput(state=new_state, result=unflat(res),
+                                      measurements=measurements)
+
+    return tc.AggregationProcess(init_fn, next_fn)
+
+
+def configure_aggregator(factory,
+                         rotation: str = "identity",
+                         concatenate: bool = True,
+                         zeroing: bool = True,
+                         clipping: bool = True,
+                         weighted: bool = True,
+                         group_layers: bool = False,
+                         task: str = ""):
+  """builder.py:37-119 (see module docstring for what is restated)."""
+  del task
+  if rotation in ("hadamard", "dft"):
+    raise NotImplementedError(
+        "rotation=%r needs the TFF HadamardTransform/DFT factories (SURVEY.md 8f row 4)" % rotation)
+  if rotation != "identity":
+    raise ValueError(
+        "Provided `rotation` must be one of 'dft', 'hadamard' or 'identity'.")
+  if group_layers:
+    raise NotImplementedError("group_layers is out of scope (SURVEY.md 2a, group.py)")
+  return WrappedAggregationFactory(factory, concatenate=concatenate, weighted=weighted,
+                                   clipping=clipping, zeroing=zeroing)
+
+
+def build_quantization_encode_aggregator(
+    step_size: float = 0.5,
+    rounding_type: str = "uniform",
+    normalization_type: str = "constant",
+    step_size_sched: str = "fixed",
+    step_size_sched_hparam: float = 0.,
+    min_step_size: float = 0.01,
+    rotation: str = "identity",
+    concatenate: bool = True,
+    zeroing: bool = True,
+    clipping: bool = True,
+    weighted: bool = True):
+  """Creates an aggregation factory for quantization and entropy coding."""
+  if rounding_type not in ["uniform", "stochastic", "dithered"]:
+    raise ValueError("Expected `rounding_type` to be one one of [\"uniform\", "
+                     f"\"stochastic\", \"dithered\"], found {rounding_type}.")
+
+  if normalization_type not in [
+      "constant", "mean_magnitude", "max_magnitude", "dimensionless_norm"
+  ]:
+    raise ValueError(
+        "Expected `normalization_type` to be one one of [\"constant\", "
+        "\"mean_magnitude\", \"max_magnitude\", \"dimensionless_norm\"], found "
+        f"{normalization_type}.")
+
+  if step_size_sched not in [
+      "fixed", "linear_decay", "exponential_decay", "step_decay"
+  ]:
+    raise ValueError(
+        "Expected `step_size_sched` to be one one of [\"fixed\", "
+        "\"linear_decay\", \"exponential_decay\", \"step_decay\"], found "
+        f"{step_size_sched}.")
+
+  factory = quantize_encode.QuantizeEncodeFactory(step_size, rounding_type,
+                                                  normalization_type,
+                                                  step_size_sched,
+                                                  step_size_sched_hparam,
+                                                  min_step_size)
+
+  return configure_aggregator(factory, rotation, concatenate, zeroing, clipping,
+                              weighted)

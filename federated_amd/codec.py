@@ -102,7 +102,7 @@ def _rows(xs, dtype):
 
 
 def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, ptrs=None,
-                    out=None, P=None):
+                    out=None, P=None, prescale=None):
   """fc_quantize_encode over a batch.  ``xs``: [C, P] tensor or list of tensors.
 
   ``seeds``: int64 tensor [C, 2] (device or host).  ``norms``: optional device
@@ -123,7 +123,7 @@ def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, p
     out = EncodedBatch(P, C, caps if caps is not None else [default_capacity(P)] * C, device)
   ws = _WS.get(C, P, device)
   _lib.call("fc_quantize_encode", _lib.ptr(ptrs), C, P, float(step), _lib.ptr(norms),
-            _lib.ptr(seeds), int(mode), _lib.ptr(out.stream), _lib.ptr(out.stream_off),
+            _lib.ptr(prescale), _lib.ptr(seeds), int(mode), _lib.ptr(out.stream), _lib.ptr(out.stream_off),
             _lib.ptr(out.stream_cap), _lib.ptr(out.idx), _lib.ptr(out.total_bits),
             _lib.ptr(out.dist_part), _lib.ptr(out.nnz_part), _lib.ptr(out.overflow),
             _lib.ptr(ws), ws.numel(), _lib.stream_handle(stream))
@@ -135,13 +135,13 @@ def check_overflow(batch):
   return np.nonzero(batch.overflow.cpu().numpy())[0]
 
 
-def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None):
+def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None, prescale=None):
   """quantize_encode, re-encoding with worst-case capacity if any client overflowed."""
   rows = _rows(xs, torch.float32)
   P = rows[0].numel()
-  batch = quantize_encode(rows, step, seeds, mode, norms=norms, caps=caps)
+  batch = quantize_encode(rows, step, seeds, mode, norms=norms, caps=caps, prescale=prescale)
   if len(check_overflow(batch)):
-    batch = quantize_encode(rows, step, seeds, mode, norms=norms,
+    batch = quantize_encode(rows, step, seeds, mode, norms=norms, prescale=prescale,
                             caps=[worst_case_capacity(P)] * len(rows))
     assert not len(check_overflow(batch))
   return batch

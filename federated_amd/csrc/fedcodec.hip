@@ -214,6 +214,7 @@ struct EncodeArgs {
   float step;
   float rcp;  // 1 / step when step is a power of two (exact reciprocal path)
   const float* norms;
+  const float* prescale;  // nullable [2*C]: x -> (x * clip) * weight before quantising
   const int64_t* seeds;
   uint8_t* stream_buf;
   const int64_t* stream_off;
@@ -411,6 +412,8 @@ __device__ __forceinline__ void load_raw(const EncodeArgs& a, uint32_t ticket, i
 struct ClientQ {
   float step;
   float rcp;
+  float s0, s1;  // pre-scales (TFF clipping factor, MeanFactory weight)
+  bool pre;
   Key4 key;
 };
 
@@ -420,6 +423,9 @@ __device__ __forceinline__ ClientQ client_q(const EncodeArgs& a, int32_t c) {
   r.step = a.step;
   if (!INT_IN && a.norms) r.step = a.norms[c] * a.step;
   r.rcp = a.rcp;
+  r.pre = !INT_IN && a.prescale != nullptr;
+  r.s0 = r.pre ? a.prescale[2 * c] : 1.0f;
+  r.s1 = r.pre ? a.prescale[2 * c + 1] : 1.0f;
   r.key = Key4{0, 0, 0, 0};
   if (!INT_IN && MODE != FC_UNIFORM) r.key = tf_seed_scramble(a.seeds[2 * c], a.seeds[2 * c + 1]);
   return r;
@@ -440,7 +446,8 @@ __device__ __forceinline__ void quant_chunk(const ClientQ& cq, int64_t e0, int64
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float deq, noise;
-      const float xv = __uint_as_float(r4[k]);
+      float xv = __uint_as_float(r4[k]);
+      if (cq.pre) xv = (xv * cq.s0) * cq.s1;  // clipping_factory, then MeanFactory weight
       const int32_t qq = quantize_one<MODE, RCP>(xv, cq.step, cq.rcp, rr[k], deq, noise);
       const bool valid = e0 + k < P;
       q4[k] = valid ? qq : 0;
@@ -1110,7 +1117,7 @@ __global__ __launch_bounds__(kThreads) void k_client_norms(const float* const* x
   for (int64_t i = threadIdx.x; i < P; i += kThreads) {
     const float v = x[i] + 0.0f;  // DAZ
     const double a = fabs((double)v);
-    if (kind == FC_NORM_MAX_MAGNITUDE) acc = a > acc ? a : acc;
+    if (kind == FC_NORM_MAX_MAGNITUDE || kind == FC_NORM_LINF) acc = a > acc ? a : acc;
     else if (kind == FC_NORM_MEAN_MAGNITUDE) acc += a;
     else acc += a * a;
   }
@@ -1119,7 +1126,8 @@ __global__ __launch_bounds__(kThreads) void k_client_norms(const float* const* x
   for (int o = kThreads / 2; o > 0; o >>= 1) {
     if (threadIdx.x < o) {
       const double b = red[threadIdx.x + o];
-      red[threadIdx.x] = (kind == FC_NORM_MAX_MAGNITUDE) ? fmax(red[threadIdx.x], b) : red[threadIdx.x] + b;
+      red[threadIdx.x] = (kind == FC_NORM_MAX_MAGNITUDE || kind == FC_NORM_LINF) ? fmax(red[threadIdx.x], b)
+                                                                               : red[threadIdx.x] + b;
     }
     __syncthreads();
   }
@@ -1127,6 +1135,7 @@ __global__ __launch_bounds__(kThreads) void k_client_norms(const float* const* x
     double r = red[0];
     if (kind == FC_NORM_MEAN_MAGNITUDE) r = r / (double)P;
     if (kind == FC_NORM_DIMENSIONLESS) r = sqrt(r / (double)P);
+    if (kind == FC_NORM_L2) r = sqrt(r);
     norms[c] = (float)r;
   }
 }
@@ -1258,7 +1267,7 @@ int64_t tiles_for(int64_t P) { return (P + kTE - 1) / kTE; }
 int64_t enc_status_bytes(int32_t n, int64_t P) { return ((int64_t)n * tiles_for(P) * 16 + 64 + 255) & ~255LL; }
 
 int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step, const float* norms,
-                  const int64_t* seeds, int mode, bool int_in, uint8_t* stream_buf,
+                  const float* prescale, const int64_t* seeds, int mode, bool int_in, uint8_t* stream_buf,
                   const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
                   int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow,
                   void* workspace, int64_t workspace_bytes, void* stream) {
@@ -1284,6 +1293,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   a.T = (int32_t)T;
   a.step = step;
   a.norms = norms;
+  a.prescale = int_in ? nullptr : prescale;
   a.seeds = seeds;
   a.stream_buf = stream_buf;
   a.stream_off = stream_off;
@@ -1363,11 +1373,11 @@ int fc_quantize(const float* x, int64_t P, float step, int64_t seed0, int64_t se
 }
 
 int fc_quantize_encode(const float* const* xs, int32_t nclients, int64_t P, float step,
-                       const float* norms, const int64_t* seeds, int mode, uint8_t* stream_buf,
+                       const float* norms, const float* prescale, const int64_t* seeds, int mode, uint8_t* stream_buf,
                        const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
                        int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow,
                        void* workspace, int64_t workspace_bytes, void* stream) {
-  return encode_common((const void* const*)xs, nclients, P, step, norms, seeds, mode, false, stream_buf,
+  return encode_common((const void* const*)xs, nclients, P, step, norms, prescale, seeds, mode, false, stream_buf,
                        stream_off, stream_cap, idx, total_bits, dist_part, nnz_part, overflow, workspace,
                        workspace_bytes, stream);
 }
@@ -1376,7 +1386,7 @@ int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P, uin
                       const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
                       int64_t* total_bits, int32_t* overflow, void* workspace, int64_t workspace_bytes,
                       void* stream) {
-  return encode_common((const void* const*)qs, nclients, P, 1.0f, nullptr, nullptr, FC_UNIFORM, true,
+  return encode_common((const void* const*)qs, nclients, P, 1.0f, nullptr, nullptr, nullptr, FC_UNIFORM, true,
                        stream_buf, stream_off, stream_cap, idx, total_bits, nullptr, nullptr, overflow,
                        workspace, workspace_bytes, stream);
 }
@@ -1436,7 +1446,7 @@ int fc_noise_sum(const int64_t* seeds, int32_t nclients, int64_t P, float* noise
 
 int fc_client_norms(const float* const* xs, int32_t nclients, int64_t P, int kind, float* norms, void* stream) {
   if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
-  if (kind < 1 || kind > 3) return fail(-1, "bad norm kind");
+  if (kind < 1 || kind > 5) return fail(-1, "bad norm kind");
   if (!xs || !norms) return fail(-1, "null pointer");
   hipLaunchKernelGGL(k_client_norms, dim3(nclients), dim3(kThreads), 0, (hipStream_t)stream, xs, P, kind, norms);
   return check_launch("k_client_norms");

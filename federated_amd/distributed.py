@@ -1,0 +1,48 @@
+"""Client-sharded multi-GPU aggregation (one process per GPU, RCCL over xGMI).
+
+A round's clients are independent until the server sum
+(``federated_aggregate`` accumulate/merge, elias_gamma_encode.py:63-88), and
+the sum is an associative int32 sum.  So each rank encodes and decodes its
+contiguous block of clients and the ranks' int32 partial sums are combined
+with ONE all-reduce (backend "nccl" = RCCL on ROCm; "gloo" in CPU tests).
+Integer addition is exact and order-independent, so the result is bit-identical
+to the single-GPU sum for any world size or ring order.  The dequantise then
+runs once, on every rank (each rank holds the server result).
+"""
+import torch
+import torch.distributed as dist
+
+from federated_amd import _lib
+from federated_amd import codec
+
+
+def client_shard(nclients, world, rank):
+  """Contiguous block [lo, hi) of clients for `rank` (sizes differ by <= 1)."""
+  base, extra = divmod(int(nclients), int(world))
+  lo = rank * base + min(rank, extra)
+  return lo, lo + base + (1 if rank < extra else 0)
+
+
+def allreduce_sum_(t, group=None):
+  """In-place SUM all-reduce of an integer (or float) tensor; no-op at world 1."""
+  if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+  return t
+
+
+def aggregate_round(local_rows, step, local_seeds, mode, group=None, prescale=None):
+  """Encode + decode this rank's clients, all-reduce the int32 sums, dequantise.
+
+  Returns (float32 result [P], local EncodedBatch).  Dithered mode also
+  all-reduces the float32 noise sum (tolerance, as TFF's federated_sum).
+  """
+  batch = codec.quantize_encode_checked(local_rows, step, local_seeds, mode, prescale=prescale)
+  isum, _, err = codec.decode_accumulate(batch, want_sum=True)
+  if int(err.item()):
+    raise RuntimeError("malformed run-length gamma code")
+  allreduce_sum_(isum, group)
+  noise = None
+  if mode == _lib.DITHERED:
+    noise = codec.noise_sum(local_seeds, batch.P, isum.device)
+    allreduce_sum_(noise, group)
+  return codec.dequantize(isum, step, noise), batch

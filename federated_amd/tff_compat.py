@@ -83,8 +83,8 @@ class AggregationProcess:
   def initialize(self):
     return self._initialize_fn()
 
-  def next(self, state, value, *args):
-    return self._next_fn(state, value, *args)
+  def next(self, state, value, *args, **kwargs):
+    return self._next_fn(state, value, *args, **kwargs)
 
 
 class UnweightedAggregationFactory:

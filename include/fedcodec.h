@@ -54,6 +54,9 @@ extern "C" {
 #define FC_NORM_MEAN_MAGNITUDE 1
 #define FC_NORM_MAX_MAGNITUDE 2
 #define FC_NORM_DIMENSIONLESS 3
+/* Norms of the TFF wrappers restated by the builder (builder.py:104-117). */
+#define FC_NORM_L2 4   /* tf.linalg.global_norm: clipping_factory */
+#define FC_NORM_LINF 5 /* max |x|: zeroing_factory (norm_order=inf) */
 
 #define FC_TILE_ELEMS 4096       /* encoder tile = decoder index granularity */
 #define FC_MAX_ELEMS 67108863LL  /* P limit: 2^26 - 1 elements per client tensor */
@@ -77,6 +80,9 @@ int fc_quantize(const float* x, int64_t P, float step, int64_t seed0, int64_t se
 /* Fused client-side quantise + run-length-gamma encode for a batch of clients.
  *   xs          device array of nclients device pointers to float32[P]
  *   norms       nullable device float[nclients]: client step = norms[c] * step
+ *   prescale    nullable device float[2 * nclients]: x -> (x * prescale[2c]) *
+ *               prescale[2c+1] before quantising (the TFF clipping_factory scale,
+ *               then the MeanFactory client weight; builder.py:100-109)
  *   seeds       device int64[2 * nclients] (TF stateless seed per client)
  *   stream_buf  device byte buffer; client c's code starts at stream_off[c]
  *               (16-byte aligned) with room for stream_cap[c] bytes
@@ -88,7 +94,7 @@ int fc_quantize(const float* x, int64_t P, float step, int64_t seed0, int64_t se
  *               (the code is then incomplete; total_bits is still exact)
  * Bit-exact on q and on the bitstream vs the oracle's restatement. */
 int fc_quantize_encode(const float* const* xs, int32_t nclients, int64_t P, float step,
-                       const float* norms, const int64_t* seeds, int mode,
+                       const float* norms, const float* prescale, const int64_t* seeds, int mode,
                        uint8_t* stream_buf, const int64_t* stream_off,
                        const int64_t* stream_cap, uint64_t* idx, int64_t* total_bits,
                        float* dist_part, int32_t* nnz_part, int32_t* overflow,
@@ -122,7 +128,8 @@ int fc_dequantize(const int32_t* sum, int64_t P, float step, const float* noise_
 int fc_noise_sum(const int64_t* seeds, int32_t nclients, int64_t P, float* noise_sum,
                  void* stream);
 
-/* norms[c] = normalize_fn(x_c) as float32, for kind in FC_NORM_*. */
+/* norms[c] = normalize_fn(x_c) (or the wrapper norms) as float32, kind in FC_NORM_*;
+ * float64 accumulation in a fixed order. */
 int fc_client_norms(const float* const* xs, int32_t nclients, int64_t P, int kind,
                     float* norms, void* stream);
 

@@ -1,0 +1,108 @@
+"""Round semantics of the reference aggregation processes (TEST INFRASTRUCTURE ONLY).
+
+Each function restates one ``next_fn`` of compressed_communication/ in numpy +
+the C run-length-gamma restatement, for a list of client values:
+
+* ``quantize_encode_next``   aggregators/quantize_encode.py:139-211
+* ``elias_gamma_sum_next``   aggregators/elias_gamma_encode.py:63-114
+* ``stochastic_quantize_next`` aggregators/stochastic_quantize.py:57-88 (SumFactory inner)
+* ``one_bit_sgd_next``       aggregators/comparison_methods/one_bit_sgd.py:45-112
+
+Float reductions (distortion, 1-bit means, one-bit decoded sums) follow TF's
+float32 semantics up to summation order; tests compare them with tolerances.
+"""
+import collections
+
+import numpy as np
+
+from oracle import codec
+from oracle import quantize_utils as qu
+
+F32 = np.float32
+
+_Q = {"uniform": lambda x, s, seed: qu.uniform_quantize(x, s), "stochastic": qu.stochastic_quantize,
+      "dithered": qu.dithered_quantize}
+_NORM = {"constant": lambda x: F32(1.0), "mean_magnitude": qu.mean_magnitude,
+         "max_magnitude": qu.max_magnitude, "dimensionless_norm": qu.dimensionless_norm}
+
+
+def wrap_i32(a):
+  return ((np.asarray(a, np.int64) + 2**31) % 2**32 - 2**31).astype(np.int32)
+
+
+def quantize_encode_next(client_values, step_size, rounding_type="uniform", seeds=None,
+                         normalization_type="constant"):
+  """One round of QuantizeEncodeFactory: returns (result, measurements, codes)."""
+  xs = [np.asarray(v, np.float32).reshape(-1) for v in client_values]
+  P = xs[0].size
+  step_size = F32(step_size)
+  if seeds is None:
+    seeds = [(c, c) for c in range(len(xs))]
+  acc = np.zeros(P, np.int64)
+  noise_sum = np.zeros(P, np.float32)
+  dists, sps, lengths, codes = [], [], [], []
+  for c, x in enumerate(xs):
+    step = F32(_NORM[normalization_type](x) * step_size)                 # :145
+    q = _Q[rounding_type](x, step, tuple(seeds[c]))                        # :146
+    if rounding_type == "dithered":
+      noise = qu.generate_noise(tuple(seeds[c]), P)                        # :147
+      deq = qu.dithered_dequantize(q, step, noise)                         # :148-149
+      noise_sum = (noise_sum + noise).astype(np.float32)                   # :183
+    else:
+      deq = qu.uniform_dequantize(q, step)
+    d = qu.ftz(x) - deq
+    dists.append(F32(np.sum(d.astype(np.float64) ** 2) / P))             # :150-152
+    sps.append(F32((F32(P) - F32(np.count_nonzero(q))) / F32(P)))        # :153-155
+    code, _ = codec.run_length_gamma_encode(q)                             # e_g_e.py:97-99
+    codes.append(code)
+    lengths.append(codec.get_bitstring_length(code))                      # e_g_e.py:100-101
+    acc += q
+  isum = wrap_i32(acc)                                                     # e_g_e.py:63-88
+  if rounding_type == "dithered":
+    result = qu.dithered_dequantize(isum, step_size, noise_sum)           # :189-190
+  else:
+    result = qu.uniform_dequantize(isum, step_size)
+  measurements = collections.OrderedDict(
+      avg_bitrate=np.float64(np.mean(lengths) / np.float64(P)),           # e_g_e.py:102-108
+      avg_distortion=F32(np.mean(dists)),
+      avg_sparsity=F32(np.mean(sps)),
+      step_size=step_size)
+  return result, measurements, codes
+
+
+def elias_gamma_sum_next(client_values):
+  """EliasGammaEncodedSumFactory round: (int32 sum, avg_bitrate, codes)."""
+  qs = [np.asarray(v, np.int32).reshape(-1) for v in client_values]
+  acc = np.zeros(qs[0].size, np.int32)
+  codes = []
+  for q in qs:
+    code, _ = codec.run_length_gamma_encode(q)
+    codes.append(code)
+    codec.decode_accumulate(code, acc)
+  bits = [codec.get_bitstring_length(c) for c in codes]
+  return acc, np.float64(np.mean(bits) / np.float64(qs[0].size)), codes
+
+
+def stochastic_quantize_next(client_values, scale_factor, seeds):
+  qs = [qu.stochastic_quantize(np.asarray(v, np.float32), scale_factor, tuple(s))
+        for v, s in zip(client_values, seeds)]
+  s = wrap_i32(np.sum(np.stack(qs).astype(np.int64), axis=0))
+  return qu.uniform_dequantize(s, scale_factor), s
+
+
+def one_bit_sgd_next(client_values, threshold=0.0):
+  """OneBitSGDFactory round: (float32 result, measurements)."""
+  xs = [np.asarray(v, np.float32).reshape(-1) for v in client_values]
+  P = xs[0].size
+  acc = np.zeros(P, np.float32)
+  dists = []
+  for x in xs:
+    above = (x >= F32(threshold)).astype(np.float32)                        # :63-67
+    below = F32(1.0) - above
+    mb = F32(np.sum(x * below, dtype=np.float64) / max(np.sum(below), 1.0))  # :69-74
+    ma = F32(np.sum(x * above, dtype=np.float64) / max(np.sum(above), 1.0))
+    dec = (above * ma + (F32(1.0) - above) * mb).astype(np.float32)         # :45-54
+    dists.append(F32(np.sum((x - dec).astype(np.float64) ** 2) / P))
+    acc = (acc + dec).astype(np.float32)                                     # :97-100
+  return acc, collections.OrderedDict(avg_bitrate=F32((F32(P) + F32(64.0)) / F32(P)),
+                                      avg_distortion=F32(np.mean(dists)))

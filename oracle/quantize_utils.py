@@ -34,7 +34,8 @@ def f32_to_i32(v):
 
 
 def _div(value, step_size):
-  return ftz(ftz(value) / ftz(F32(step_size)))
+  with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
+    return ftz(ftz(value) / ftz(F32(step_size)))
 
 
 # quantize_utils.py:20-21
@@ -71,7 +72,8 @@ def stochastic_quantize(value, step_size, seed):
   value = np.asarray(value, np.float32).reshape(-1)
   scaled = _div(value, step_size)
   fl = np.floor(scaled)
-  prob = ftz(scaled - fl)
+  with np.errstate(invalid="ignore"):
+    prob = ftz(scaled - fl)
   rnd = philox.stateless_uniform(value.size, seed)
   rounded = np.where(rnd <= prob, np.ceil(scaled), fl)
   return f32_to_i32(rounded)
@@ -87,7 +89,8 @@ def dithered_quantize(value, step_size, seed):
   value = np.asarray(value, np.float32).reshape(-1)
   scaled = _div(value, step_size)
   noise = generate_noise(seed, value.size)
-  return f32_to_i32(np.rint(ftz(scaled - noise)))
+  with np.errstate(invalid="ignore"):
+    return f32_to_i32(np.rint(ftz(scaled - noise)))
 
 
 # quantize_utils.py:69-84

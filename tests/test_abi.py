@@ -1,0 +1,69 @@
+"""The C ABI library loads and exports every symbol include/fedcodec.h declares (no GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from federated_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+  hdr = open(os.path.join(ROOT, "include", "fedcodec.h")).read()
+  hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+  return sorted(set(re.findall(r"\b(fc_[a-z0-9_]+)\s*\(", hdr)))
+
+
+def test_header_declares_the_expected_surface():
+  syms = declared_symbols()
+  for s in ["fc_quantize", "fc_quantize_encode", "fc_rlgamma_encode", "fc_decode_accumulate",
+            "fc_dequantize", "fc_noise_sum", "fc_client_norms", "fc_finalize"]:
+    assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+  lib = _lib.load()
+  for s in declared_symbols():
+    assert hasattr(lib, s), s
+    assert s in _lib.SIGNATURES, "ctypes signature missing for %s" % s
+
+
+def test_host_only_entry_points():
+  lib = _lib.load()
+  assert lib.fc_version().startswith(b"fedcodec")
+  assert lib.fc_num_tiles(25_000_000) == 6104
+  assert lib.fc_num_tiles(0) == 0
+  assert lib.fc_encode_workspace_bytes(128, 25_000_000) >= 128 * 6104 * 16
+
+
+def test_argument_validation_without_gpu():
+  lib = _lib.load()
+  # rejected before any device work: bad sizes / null pointers / bad mode
+  rc = lib.fc_quantize_encode(None, 0, 10, 1.0, None, None, None, 0, None, None, None, None, None,
+                              None, None, None, None, 0, None)
+  assert rc != 0 and b"nclients" in lib.fc_last_error()
+  rc = lib.fc_quantize(None, 10, 1.0, 0, 0, 7, None, None, None)
+  assert rc != 0
+  rc = lib.fc_client_norms(None, 1, 10, 9, None, None)
+  assert rc != 0 and b"norm" in lib.fc_last_error()
+  rc = lib.fc_decode_accumulate(None, None, None, None, 1, (1 << 26), None, None, None, 1.0, None,
+                                None, None)
+  assert rc != 0
+
+
+def test_product_package_never_imports_the_oracle():
+  pkg = os.path.join(ROOT, "federated_amd")
+  for dirpath, _, files in os.walk(pkg):
+    for f in files:
+      if f.endswith(".py"):
+        src = open(os.path.join(dirpath, f)).read()
+        assert "import oracle" not in src and "from oracle" not in src, f
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+  monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+  monkeypatch.setattr(_lib, "_lib", None)
+  with pytest.raises(_lib.FedCodecError):
+    _lib.load()

@@ -1,0 +1,122 @@
+"""Reference-shaped API surface, host-side logic only (no GPU).
+
+Mirrors the ComputationTest halves of the reference tests: constructor
+validation, create() type checks, initialize() state structure.
+"""
+import collections
+
+import numpy as np
+import pytest
+
+from federated_amd import builder
+from federated_amd import tff_compat as tc
+from federated_amd.aggregators import elias_gamma_encode
+from federated_amd.aggregators import quantize_encode
+from federated_amd.aggregators import stochastic_quantize
+from federated_amd.aggregators import sum_factory
+from federated_amd.aggregators.comparison_methods import one_bit_sgd
+from federated_amd.aggregators.utils import quantize_utils
+
+
+# quantize_encode_test.py:30-65
+@pytest.mark.parametrize("rounding", ["uniform", "stochastic", "dithered"])
+def test_quantize_encode_initialize_state(rounding):
+  process = quantize_encode.QuantizeEncodeFactory(1.0, rounding_type=rounding).create(
+      (np.float32, (3,)))
+  state = process.initialize()
+  assert isinstance(state, collections.OrderedDict)
+  assert list(state) == ["round_num", "step_size", "inner_state"]
+  assert state["round_num"].dtype == np.float32 and state["round_num"] == 0.0
+  assert state["step_size"].dtype == np.float32 and state["step_size"] == 1.0
+  assert state["inner_state"] == ()
+
+
+# quantize_encode_test.py:136-146
+@pytest.mark.parametrize("value_type", [(np.int32, (3,)), [(np.float32, (2,)), (np.float32, (3,))]])
+def test_quantize_encode_create_raises(value_type):
+  with pytest.raises(ValueError):
+    quantize_encode.QuantizeEncodeFactory(1.0).create(value_type)
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(rounding_type="bogus"), "rounding_type"),
+    (dict(normalization_type="bogus"), "normalization_type"),
+    (dict(schedule="bogus"), "schedule"),
+])
+def test_quantize_encode_ctor_raises(kw, msg):
+  with pytest.raises(ValueError, match=msg):
+    quantize_encode.QuantizeEncodeFactory(0.5, **kw)
+
+
+# elias_gamma_encode_test.py:40-77
+def test_elias_gamma_create():
+  process = elias_gamma_encode.EliasGammaEncodedSumFactory().create((np.int32, (4,)))
+  assert process.initialize() == ()
+  for bad in [(np.float32, (3,)), [(np.int32, (2,)), (np.int32, (3,))]]:
+    with pytest.raises(ValueError):
+      elias_gamma_encode.EliasGammaEncodedSumFactory().create(bad)
+  assert elias_gamma_encode.get_bitstring_length(b"ab") == 16.0
+
+
+def test_stochastic_quantize_create():
+  f = stochastic_quantize.StochasticQuantizeFactory(0.4, sum_factory.add_sum_measurements())
+  assert f.create((np.float32, (3,))).initialize() == ()
+  with pytest.raises(ValueError):
+    f.create((np.int32, (3,)))
+
+
+def test_one_bit_create():
+  assert one_bit_sgd.OneBitSGDFactory().create((np.float32, (3,))).initialize() == ()
+  with pytest.raises(ValueError):
+    one_bit_sgd.OneBitSGDFactory().create((np.int32, (3,)))
+
+
+# builder_test.py / builder.py:498-516
+@pytest.mark.parametrize("kw,msg", [
+    (dict(rounding_type="x"), "rounding_type"),
+    (dict(normalization_type="x"), "normalization_type"),
+    (dict(step_size_sched="x"), "step_size_sched"),
+])
+def test_builder_validation(kw, msg):
+  with pytest.raises(ValueError, match=msg):
+    builder.build_quantization_encode_aggregator(**kw)
+
+
+def test_builder_default_state():
+  f = builder.build_quantization_encode_aggregator(rounding_type="stochastic", zeroing=False)
+  process = f.create([(np.float32, (2, 3)), (np.float32, (4,))], (np.float32, ()))
+  state = process.initialize()
+  assert state["clipping_norm"] == np.float32(1.0)
+  assert state["zeroing_norm"] == ()
+  assert list(state["inner_state"]) == ["round_num", "step_size", "inner_state"]
+  with pytest.raises(ValueError):
+    builder.configure_aggregator(quantize_encode.QuantizeEncodeFactory(0.5), rotation="bogus")
+
+
+def test_quantile_estimate_geometric_update():
+  q = builder.QuantileEstimate(1.0, 0.8, 0.2)
+  # all norms below the estimate -> estimate shrinks by exp(-0.2 * 0.2)
+  assert np.isclose(q.update(np.float32(1.0), [0.1, 0.2]), np.exp(-0.2 * 0.2), rtol=1e-6)
+  z = builder.QuantileEstimate(10.0, 0.98, np.log(10.0), multiplier=2.0, increment=1.0)
+  assert z.report(np.float32(10.0)) == 21.0
+
+
+# quantize_utils_test.py:157-186 (host scalar schedules of the product package)
+def test_product_schedules():
+  assert [float(quantize_utils.linear_decay(2., 0., r, 4)) for r in range(4)] == [2., 1.5, 1., 0.5]
+  assert [float(quantize_utils.step_decay(2., 0., r, 2)) for r in range(4)] == [2., 2., 1., 1.]
+  np.testing.assert_allclose([quantize_utils.exponential_decay(2., 0., r, 1.) for r in range(4)],
+                             [2., 2. * np.exp(-1.), 2. * np.exp(-2.), 2. * np.exp(-3.)], rtol=1e-6)
+
+
+def test_schedule_state_update_is_host_side():
+  f = quantize_encode.QuantizeEncodeFactory(2.0, schedule="step_decay", schedule_hparam=2,
+                                            min_step_size=0.1)
+  assert f._schedule_fn(np.float32(3.0)) == np.float32(1.0)
+
+
+def test_to_type():
+  t = tc.to_type((np.float32, (2, 4)))
+  assert t.num_elements == 8 and t.is_tensor()
+  s = tc.to_type([(np.float32, (2,)), (np.int32, (3,))])
+  assert not s.is_tensor() and not tc.is_structure_of_floats(s)

@@ -1,0 +1,183 @@
+"""GPU parity of the reference-shaped aggregation processes (ExecutionTest halves).
+
+Each case mirrors a reference execution test (file:line) and additionally
+checks bit-exactness against the CPU oracle on seeded inputs and the committed
+golden fixtures.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from federated_amd import _lib
+from federated_amd import builder
+from federated_amd import codec
+from federated_amd.aggregators import elias_gamma_encode
+from federated_amd.aggregators import quantize_encode
+from federated_amd.aggregators import stochastic_quantize
+from federated_amd.aggregators import sum_factory
+from federated_amd.aggregators.comparison_methods import one_bit_sgd
+from federated_amd.aggregators.utils import quantize_utils
+from oracle import aggregators as oagg
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden.npz")
+SEEDS = [(0, 0), (1, 1), (2**40 + 7, 3)]
+
+
+# quantize_encode_test.py:154-206
+@pytest.mark.parametrize("rounding", ["uniform", "stochastic"])
+def test_quantize_encode_reference_execution(gpu, rounding):
+  process = quantize_encode.QuantizeEncodeFactory(1.0, rounding_type=rounding).create(
+      (np.float32, (3,)))
+  out = process.next(process.initialize(), [np.ones(3, np.float32)] * 2)
+  np.testing.assert_array_equal(out.result, [2.0, 2.0, 2.0])
+  m = out.measurements
+  assert m["avg_bitrate"] == np.float64(16.0 / 3.0)
+  assert m["avg_distortion"] == 0.0 and m["avg_sparsity"] == 0.0 and m["step_size"] == 1.0
+  assert out.state["round_num"] == 1.0 and out.state["step_size"] == 1.0
+
+
+# quantize_encode_test.py:211-226
+def test_quantize_encode_dithered_execution(gpu):
+  process = quantize_encode.QuantizeEncodeFactory(1.0, rounding_type="dithered").create(
+      (np.float32, (3,)))
+  out = process.next(process.initialize(), [np.ones(3, np.float32)] * 2)
+  assert np.max(np.abs(out.result - 2.0)) <= 1.0
+
+
+@pytest.mark.parametrize("rounding", ["uniform", "stochastic", "dithered"])
+def test_quantize_encode_matches_golden_round(gpu, rounding):
+  g = np.load(GOLDEN, allow_pickle=False)
+  xs = list(g["round_x"])
+  process = quantize_encode.QuantizeEncodeFactory(0.5, rounding_type=rounding).create(
+      (np.float32, (xs[0].size,)))
+  out = process.next(process.initialize(), xs, seeds=np.array(SEEDS))
+  np.testing.assert_array_equal(out.result, g["round_%s_result" % rounding])
+  assert out.measurements["avg_bitrate"] == g["round_%s_bitrate" % rounding]
+  np.testing.assert_allclose(out.measurements["avg_distortion"], g["round_%s_distortion" % rounding],
+                             rtol=1e-5)
+  assert out.measurements["avg_sparsity"] == g["round_%s_sparsity" % rounding]
+
+
+@pytest.mark.parametrize("norm", ["mean_magnitude", "max_magnitude", "dimensionless_norm"])
+def test_quantize_encode_normalized_matches_oracle(gpu, norm):
+  rng = np.random.default_rng(5)
+  xs = [(rng.standard_normal(4097) * (c + 1)).astype(np.float32) for c in range(3)]
+  process = quantize_encode.QuantizeEncodeFactory(0.25, rounding_type="stochastic",
+                                                  normalization_type=norm).create(
+                                                      (np.float32, (4097,)))
+  out = process.next(process.initialize(), xs, seeds=np.array(SEEDS))
+  want, meas, _ = oagg.quantize_encode_next(xs, 0.25, "stochastic", seeds=SEEDS,
+                                            normalization_type=norm)
+  if norm == "max_magnitude":  # exact reduction -> bit-exact
+    np.testing.assert_array_equal(out.result, want)
+  else:  # float reduction order of the norm: tolerance on the result (quantisation may flip)
+    assert np.mean(out.result != want) < 0.01
+  np.testing.assert_allclose(out.measurements["avg_bitrate"], meas["avg_bitrate"], rtol=0.01)
+
+
+def test_elias_gamma_factory_reference_execution(gpu):
+  # elias_gamma_encode_test.py:80-116
+  process = elias_gamma_encode.EliasGammaEncodedSumFactory().create((np.int32, (4,)))
+  out = process.next((), [[-5, 3, 0, 0], [-3, 1, 0, 0]])
+  np.testing.assert_array_equal(out.result, [-8, 4, 0, 0])
+  assert out.measurements["avg_bitrate"] == 16 / 4
+  process2 = elias_gamma_encode.EliasGammaEncodedSumFactory().create((np.int32, (2, 4)))
+  out2 = process2.next((), [[[-5, 3, 0, 0], [-3, 1, 0, 0]]] * 2)
+  np.testing.assert_array_equal(out2.result, [[-10, 6, 0, 0], [-6, 2, 0, 0]])
+  assert out2.measurements["avg_bitrate"] == 32 / 8
+
+
+def test_stochastic_quantize_reference_execution(gpu):
+  # stochastic_quantize_test.py:86-110
+  f = stochastic_quantize.StochasticQuantizeFactory(0.4, sum_factory.add_sum_measurements())
+  process = f.create((np.float32, (3,)))
+  out = process.next((), [np.full(3, 2.0, np.float32)] * 2)
+  np.testing.assert_array_equal(out.measurements, [10, 10, 10])
+  np.testing.assert_allclose(out.result, [4.0] * 3, rtol=1e-6)
+  ps = f.create([(np.float32, (2,)), (np.float32, (3,))])
+  out = ps.next((), [[np.full(2, 2.0, np.float32), np.full(3, 2.0, np.float32)]] * 2)
+  np.testing.assert_allclose(out.result[1], [4.0] * 3, rtol=1e-6)
+
+
+# one_bit_sgd_test.py:100-202
+@pytest.mark.parametrize("values,thr,want,dist", [
+    ([[-1.0] * 3] * 2, 0.0, [-2.0] * 3, 0.0),
+    ([[0.0, 2.0, -1.0]] * 2, 0.0, [2.0, 2.0, -2.0], 2. / 3.),
+    ([[-1.0, 1.0, 2.0]] * 2, 2.0, [0.0, 0.0, 4.0], 2. / 3.),
+    ([[-1.0, 1.0, 2.0]], 2.0, [0.0, 0.0, 2.0], 2. / 3.),
+    ([[-1.0, 1.0, 2.0], [1.0, 1.0, 1.0]], 2.0, [1.0, 1.0, 3.0], 2. / 6.),
+])
+def test_one_bit_sgd_reference_execution(gpu, values, thr, want, dist):
+  process = one_bit_sgd.OneBitSGDFactory(thr).create((np.float32, (3,)))
+  out = process.next((), [np.array(v, np.float32) for v in values])
+  np.testing.assert_allclose(out.result, want, rtol=1e-6, atol=1e-6)
+  np.testing.assert_allclose(out.measurements["avg_distortion"], dist, rtol=1e-6)
+  assert out.measurements["avg_bitrate"] == np.float32(67 / 3)
+
+
+def test_one_bit_matches_golden(gpu):
+  g = np.load(GOLDEN, allow_pickle=False)
+  xs = list(g["round_x"])
+  out = one_bit_sgd.OneBitSGDFactory(0.1).create((np.float32, (xs[0].size,))).next((), xs)
+  np.testing.assert_allclose(out.result, g["onebit_result"], rtol=1e-6, atol=1e-6)
+  np.testing.assert_allclose(out.measurements["avg_distortion"], g["onebit_distortion"], rtol=1e-5)
+
+
+def test_quantize_utils_device_functions(gpu):
+  # quantize_utils_test.py:46-59
+  q = quantize_utils.uniform_quantize(torch.full((3,), 2.0), 0.4, (0, 0))
+  np.testing.assert_array_equal(q.cpu().numpy(), [5, 5, 5])
+  d = quantize_utils.uniform_dequantize(torch.full((3,), 5, dtype=torch.int32), 0.4)
+  np.testing.assert_allclose(d.cpu().numpy(), [2.0] * 3, rtol=1e-7)
+  assert float(quantize_utils.max_magnitude(torch.tensor([0.0, 1.0, 2.0]))) == 2.0
+  np.testing.assert_allclose(float(quantize_utils.mean_magnitude(torch.tensor([0.0, 1.0, 2.0]))), 1.0)
+  noise = quantize_utils.generate_noise((3, 9), (1001,))
+  g = np.load(GOLDEN, allow_pickle=False)
+  np.testing.assert_array_equal(noise.cpu().numpy(), g["noise_3_9"])
+
+
+def test_quantizer_matches_golden_fixtures(gpu):
+  g = np.load(GOLDEN, allow_pickle=False)
+  x = torch.from_numpy(g["q_x"]).cuda()
+  steps = [0.5, 0.4, 1.0 / 127, 1.0]
+  for mi, m in enumerate(["uniform", "stochastic", "dithered"]):
+    for si, s in enumerate(steps):
+      for ki, sd in enumerate(SEEDS):
+        q, _ = codec.quantize(x, np.float32(s), sd, mi)
+        np.testing.assert_array_equal(q.cpu().numpy(), g["q_%s_%d_%d" % (m, si, ki)])
+
+
+def test_rlgamma_matches_golden_fixtures(gpu):
+  g = np.load(GOLDEN, allow_pickle=False)
+  names = [k[6:] for k in g.files if k.startswith("rl_in_")]
+  for name in names:
+    b = codec.rlgamma_encode([torch.from_numpy(g["rl_in_" + name]).cuda()])
+    assert int(b.bits()[0]) == int(g["rl_bits_" + name]), name
+    assert b.client_code(0) == g["rl_code_" + name].tobytes(), name
+
+
+def test_builder_round_runs_and_clips(gpu):
+  f = builder.build_quantization_encode_aggregator(step_size=0.01, rounding_type="uniform")
+  process = f.create([(np.float32, (2, 3)), (np.float32, (4,))], (np.float32, ()))
+  state = process.initialize()
+  rng = np.random.default_rng(9)
+  values = [[rng.standard_normal((2, 3)).astype(np.float32) * 0.1,
+             rng.standard_normal(4).astype(np.float32) * 0.1] for _ in range(4)]
+  weights = [1.0, 2.0, 3.0, 4.0]
+  out = process.next(state, values, weights, seeds=np.array([[i, i] for i in range(4)]))
+  # weighted mean of clipped values (norms < 1 => unclipped), quantised with step 0.01
+  flat = [np.concatenate([v[0].reshape(-1), v[1]]) for v in values]
+  want = sum(w * x for w, x in zip(weights, flat)) / sum(weights)
+  got = np.concatenate([out.result[0].reshape(-1), out.result[1]])
+  assert np.max(np.abs(got - want)) <= 0.01 * 0.5 * 4 / sum(weights) + 1e-6
+  assert out.state["clipping_norm"] != state["clipping_norm"]
+
+
+def test_decoder_rejects_malformed_stream(gpu):
+  b = codec.rlgamma_encode([torch.tensor([5, 0, -3, 7], dtype=torch.int32, device="cuda")])
+  b.stream.zero_()  # a run of zeros longer than 31 bits is not a gamma code
+  _, _, err = codec.decode_accumulate(b)
+  assert int(err.item()) != 0
