@@ -17,7 +17,7 @@ for f in sorted(glob.glob(os.path.join(out, "kt", "**", "*kernel_stats.csv"), re
             float(row["TotalDurationNs"]) / 1e6, row.get("Percentage", "")))
 agg = defaultdict(lambda: defaultdict(float))
 cnt = defaultdict(int)
-for f in sorted(glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True)):
+for f in sorted(glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)):
   with open(f) as fh:
     for row in csv.DictReader(fh):
       name = row.get("Kernel_Name", "")
