@@ -11,7 +11,7 @@ LIB_PATH = os.environ.get("FEDCODEC_LIB") or os.path.join(_HERE, "libfedcodec.so
 
 UNIFORM, STOCHASTIC, DITHERED = 0, 1, 2
 NORM_MEAN_MAGNITUDE, NORM_MAX_MAGNITUDE, NORM_DIMENSIONLESS, NORM_L2, NORM_LINF = 1, 2, 3, 4, 5
-TILE_ELEMS = 4096
+TILE_ELEMS = 1024
 MAX_ELEMS = (1 << 26) - 1
 
 # (name, restype, argtypes); every symbol declared in include/fedcodec.h.

@@ -26,12 +26,28 @@
 
 #include "../../include/fedcodec.h"
 
+// Diagnostic ablation bits (performance experiments only; 0 in every real build):
+//   1 skip LDS emission  2 skip stream stores  4 skip look-back  8 skip quantise math
+#ifndef FC_ENC_WAVES
+#define FC_ENC_WAVES 5  // encoder waves per SIMD the register budget is sized for
+#endif
+#ifndef FC_ABL
+#define FC_ABL 0
+#endif
+
 namespace {
 
 constexpr int kTE = FC_TILE_ELEMS;  // elements per tile
-constexpr int kThreads = 256;       // 4 waves of 64
-constexpr int kWinWords = 2048;     // LDS bit window (64 Kbit = 16 bits/element)
+constexpr int kThreads = 256;       // 4 waves of 64 (decoder and small kernels)
+constexpr int kEncThreads = 64;     // encoder workgroup = one wavefront = one tile at a time
+constexpr int kChunks = kTE / (4 * kEncThreads);  // 4 chunks of 4 elements per lane
+constexpr int kWinWords = 544;      // per-wave LDS bit window (17 Kbit, ~16.9 bits/element)
 constexpr uint32_t kNoPos = 0x1FFF; // "no nonzero" in a 13-bit tile-relative field
+// Ticket streams: one device-scope atomic word saturates near 90 dequeues/us
+// (MI355X_MICROARCH.md "dequeue"), so tickets come from kTicketShards counters,
+// one 64-B line each; stream k hands out tickets k, k + K, k + 2K, ... in order.
+constexpr int kTicketShards = 32;
+constexpr int kShardStride = 16;  // uint32 words between counters (64 B)
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 and TF's stateless seed scramble (see oracle/philox.py).
@@ -148,6 +164,7 @@ __device__ __forceinline__ Seg seg_combine(const Seg& a, const Seg& b) {
 //  w2: [63:62] flag  [31:0] tail
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagPre = 2ull << 62;
+constexpr uint64_t kFlagSlow = 3ull << 62;  // tile left to the exact kernel (terminal)
 constexpr uint64_t kMask36 = (1ull << 36) - 1;
 
 __device__ __forceinline__ Seg seg_from_status(uint64_t w1, uint64_t w2, int64_t tile_base) {
@@ -225,29 +242,14 @@ struct EncodeArgs {
   int32_t* nnz_part;
   int32_t* overflow;
   uint64_t* status;   // [nclients * T][2]
-  uint32_t* counter;  // ticket counter (zeroed per launch)
+  uint32_t* counter;  // kTicketShards ticket counters, 64 B apart (zeroed per launch)
+  uint32_t nshards;   // ticket streams in use: min(kTicketShards, grid)
   uint32_t* spin_err;
-};
-
-struct EncShared {
-  uint32_t win[kWinWords];  // LDS bit window (MSB-first words)
-  int32_t wave_last[4];
-  int32_t wave_first[4];
-  uint32_t wave_bits[4];
-  float wave_dist[4];
-  int32_t wave_nnz[4];
-  uint32_t tail;
-  uint32_t ticket;
-  uint32_t next_ticket;
-  uint32_t slow;  // tile needs the slow (re-quantise) emission path
-  // look-back results broadcast to the workgroup
-  uint64_t b0;
-  int32_t last_before;
-  uint32_t tail_before;
-  uint32_t r0_R0;      // stream-window bit where the body starts = (b0 % 32) + R0
-  uint32_t nwin_bits;  // bits in the stream window (incl. trailing code on the last tile)
-  uint64_t trail;      // trailing run code value
-  uint32_t trail_len;
+  const void* cparams;   // ClientParam[nclients] (workspace)
+  uint32_t* slow_count;  // clients handed to the exact kernel
+  int32_t* slow_flag;    // [nclients] (zeroed per launch)
+  int32_t* slow_list;    // [nclients]
+  uint32_t* counter2;    // exact kernel's ticket counter
 };
 
 // Emit a piece of <= 32 bits at window bit position wp into the LDS window
@@ -327,11 +329,31 @@ __device__ __forceinline__ int32_t dpp_shr1(int32_t x, int32_t fill) {  // wave_
   return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xf, 0xf, false);
 }
 __device__ __forceinline__ int32_t lane63(int32_t x) { return __builtin_amdgcn_readlane(x, 63); }
+// Whole-wave reductions through the inclusive DPP scans (no ds_bpermute address registers).
+__device__ __forceinline__ float wave_sum_f(float x) {
+  uint32_t b = __float_as_uint(x);
+  float v = x;
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, b, 0x111, 0xf, 0xf, false));
+  b = __float_as_uint(v);
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, b, 0x112, 0xf, 0xf, false));
+  b = __float_as_uint(v);
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, b, 0x114, 0xf, 0xf, false));
+  b = __float_as_uint(v);
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, b, 0x118, 0xf, 0xf, false));
+  b = __float_as_uint(v);
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, b, 0x142, 0xa, 0xf, false));
+  b = __float_as_uint(v);
+  v += __uint_as_float(__builtin_amdgcn_update_dpp(0u, b, 0x143, 0xc, 0xf, false));
+  return __uint_as_float((uint32_t)lane63((int32_t)__float_as_uint(v)));
+}
+__device__ __forceinline__ int32_t wave_sum_i(int32_t x) { return lane63((int32_t)dpp_incl_sum((uint32_t)x)); }
+__device__ __forceinline__ int32_t wave_min_i(int32_t x) { return -lane63(dpp_incl_max(-x)); }
+__device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // Decoupled look-back for tile t of one client, run by one full wave.  Returns
 // the exclusive prefix (a root segment: body = stream bits before tile t).
 __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int lane,
-                                        uint32_t* spin_err) {
+                                        uint32_t* spin_err, bool& slow) {
   Seg S = seg_identity();
   int64_t base = (int64_t)t - 1;
   for (;;) {
@@ -346,7 +368,7 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
         w2 = ld_agent(status_c + 2 * ti + 1);
         valid = (w1 >> 62) != 0 && (w1 >> 62) == (w2 >> 62);
       }
-      const uint64_t pre = __ballot(valid && (w1 >> 62) == 2);
+      const uint64_t pre = __ballot(valid && (w1 >> 62) >= 2);  // prefix or slow: terminal
       const uint64_t val = __ballot(valid);
       k = pre ? __builtin_ctzll(pre) : 64;
       const uint64_t need = k >= 63 ? ~0ull : ((2ull << k) - 1);
@@ -360,26 +382,22 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
         break;
       }
     }
-    Seg v = (lane <= k && ti >= -1) ? seg_from_status(w1, w2, ti * kTE) : seg_identity();
-    // suffix scan over lanes 0..k: lane 0 ends with the combination of the window
+    // fold lanes k (farthest, or 63) .. 0 (nearest) serially in scalar registers
+    Seg W = seg_identity();
     const int kk = k < 63 ? k : 63;
-    for (int d = 1; d <= kk; d <<= 1) {
-      Seg o;
-      o.has_nz = __shfl_down(v.has_nz, d, 64);
-      o.first = __shfl_down(v.first, d, 64);
-      o.last = __shfl_down(v.last, d, 64);
-      o.body = __shfl_down(v.body, d, 64);
-      o.tail = __shfl_down(v.tail, d, 64);
-      if (lane + d >= 64) o.has_nz = 0;
-      v = seg_combine(o, v);
+    const uint32_t w1lo = (uint32_t)w1, w1hi = (uint32_t)(w1 >> 32), w2lo = (uint32_t)w2,
+                   w2hi = (uint32_t)(w2 >> 32);
+    if (k < 64 && (__builtin_amdgcn_readlane(w1hi, k) >> 30) == 3u) {  // a slow tile: give up
+      slow = true;
+      return S;
     }
-    Seg W;
-    W.has_nz = __builtin_amdgcn_readfirstlane(v.has_nz);
-    W.first = __builtin_amdgcn_readfirstlane(v.first);
-    W.last = __builtin_amdgcn_readfirstlane(v.last);
-    W.body = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v.body >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)v.body);
-    W.tail = __builtin_amdgcn_readfirstlane(v.tail);
+    for (int i = kk; i >= 0; --i) {
+      const int64_t tii = base - i;
+      if (tii < -1) continue;
+      const uint64_t a1 = ((uint64_t)__builtin_amdgcn_readlane(w1hi, i) << 32) | __builtin_amdgcn_readlane(w1lo, i);
+      const uint64_t a2 = ((uint64_t)__builtin_amdgcn_readlane(w2hi, i) << 32) | __builtin_amdgcn_readlane(w2lo, i);
+      W = seg_combine(W, seg_from_status(a1, a2, tii * kTE));
+    }
     S = seg_combine(W, S);
     if (k < 64) break;
     base -= 64;
@@ -387,26 +405,13 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
   return S;
 }
 
-// Raw 4x4 input words (float or int32 bit patterns) of one thread's chunks.
-template <bool INT_IN>
-__device__ __forceinline__ void load_raw(const EncodeArgs& a, uint32_t ticket, int wv, int lane,
-                                         uint32_t (&raw)[4][4]) {
-  const int32_t t = (int32_t)(ticket / (uint32_t)a.nclients);
-  const int32_t c = (int32_t)(ticket - (uint32_t)t * (uint32_t)a.nclients);
-  const int64_t tile_base = (int64_t)t * kTE;
-  const uint32_t* xp = (const uint32_t*)a.xs[c];
-  const bool aligned = (((uintptr_t)xp) & 15) == 0;
+// Runtime-indexed read of a small register array without scratch (select chain).
+template <typename T, int N>
+__device__ __forceinline__ T pick(const T (&arr)[N], int j) {
+  T v = arr[0];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t e0 = tile_base + 1024 * wv + 256 * j + 4 * lane;
-    if (aligned && e0 + 3 < a.P) {
-      const uint4 v = *(const uint4*)(xp + e0);
-      raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) raw[j][k] = (e0 + k < a.P) ? xp[e0 + k] : 0u;
-    }
-  }
+  for (int i = 1; i < N; ++i) v = (j == i) ? arr[i] : v;
+  return v;
 }
 
 struct ClientQ {
@@ -416,20 +421,6 @@ struct ClientQ {
   bool pre;
   Key4 key;
 };
-
-template <int MODE, bool INT_IN>
-__device__ __forceinline__ ClientQ client_q(const EncodeArgs& a, int32_t c) {
-  ClientQ r;
-  r.step = a.step;
-  if (!INT_IN && a.norms) r.step = a.norms[c] * a.step;
-  r.rcp = a.rcp;
-  r.pre = !INT_IN && a.prescale != nullptr;
-  r.s0 = r.pre ? a.prescale[2 * c] : 1.0f;
-  r.s1 = r.pre ? a.prescale[2 * c + 1] : 1.0f;
-  r.key = Key4{0, 0, 0, 0};
-  if (!INT_IN && MODE != FC_UNIFORM) r.key = tf_seed_scramble(a.seeds[2 * c], a.seeds[2 * c + 1]);
-  return r;
-}
 
 // Quantise one chunk of 4 consecutive elements starting at e0.
 template <int MODE, bool INT_IN, bool RCP>
@@ -497,6 +488,73 @@ __device__ __forceinline__ ChunkCode chunk_local(const int32_t (&q4)[4], int32_t
   return r;
 }
 
+// Fused quantise + chunk-local code of one chunk of 4 in-range float
+// elements (the fast path's inner loop).  The rounded value stays a float (an
+// exact integer when |r| < 8192): m = |r| by one conversion, floor(log2 m) is
+// its exponent, and the in-chunk run lengths come from select chains on the
+// nonzero flags.  |r| >= 8192, Inf or NaN marks the chunk long; the slow path
+// then recomputes the tile exactly (TF cast semantics, codes of any length).
+template <int MODE, bool RCP, bool MASK = false>
+__device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t g,
+                                                     const uint32_t (&r4)[4], int32_t rel0,
+                                                     float& dist, int32_t& nnz, int32_t nvalid = 4) {
+  uint4 rb = make_uint4(0, 0, 0, 0);
+  if (MODE != FC_UNIFORM) rb = philox_group(cq.key, g);
+  const uint32_t rbits[4] = {rb.x, rb.y, rb.z, rb.w};
+  float q[4];
+  bool nz[4];
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float xv = __uint_as_float(r4[k]);
+    if (cq.pre) xv = (xv * cq.s0) * cq.s1;
+    const float sc = RCP ? xv * cq.rcp : xv / cq.step;
+    float r, noise = 0.0f;
+    if (MODE == FC_UNIFORM) {
+      r = rintf(sc);
+    } else if (MODE == FC_STOCHASTIC) {
+      const float fl = floorf(sc);
+      r = (u01(rbits[k]) <= sc - fl) ? ceilf(sc) : fl;
+    } else {
+      noise = u01(rbits[k]) - 0.5f;
+      r = rintf(sc - noise);
+    }
+    bad |= !(fabsf(r) < 8192.0f);
+    const float deq = (MODE == FC_DITHERED) ? (r + noise) * cq.step : r * cq.step;
+    const float dd = xv - deq;
+    // zero padding past P quantises to 0; only dithering's noise would count
+    dist = (!MASK || k < nvalid) ? fmaf(dd, dd, dist) : dist;
+    q[k] = r;
+    nz[k] = r != 0.0f;
+    nnz += nz[k] ? 1 : 0;
+  }
+  // run code (value dv in rl bits) before element k, from the previous nonzero in the chunk
+  const uint32_t dv1 = nz[0] ? 1u : 0u;
+  const uint32_t dv2 = nz[1] ? 1u : (nz[0] ? 2u : 0u);
+  const uint32_t rl2 = nz[1] ? 1u : (nz[0] ? 3u : 0u);
+  const uint32_t dv3 = nz[2] ? 1u : (nz[1] ? 2u : (nz[0] ? 3u : 0u));
+  const uint32_t rl3 = nz[2] ? 1u : ((nz[1] || nz[0]) ? 3u : 0u);
+  const uint32_t dv[4] = {0u, dv1, dv2, dv3};
+  const uint32_t rl[4] = {0u, dv1, rl2, rl3};
+  ChunkCode r;
+  r.acc = 0;
+  r.len = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t m = (uint32_t)fabsf(q[k]);
+    const uint32_t ml = 2u * ((__float_as_uint(q[k]) >> 23) & 0xFFu) - 253u;  // 2 floor(log2 m) + 1
+    const uint32_t t = 2u * dv[k] + (q[k] > 0.0f ? 1u : 0u);                     // run code, sign bit
+    const uint32_t code = nz[k] ? ((t << ml) | m) : 0u;
+    const uint32_t L = nz[k] ? rl[k] + ml + 1u : 0u;
+    r.acc = k == 0 ? (uint64_t)code : ((r.acc << L) | code);
+    r.len += L;
+  }
+  r.first = nz[0] ? rel0 : (nz[1] ? rel0 + 1 : (nz[2] ? rel0 + 2 : (nz[3] ? rel0 + 3 : -1)));
+  r.last = nz[3] ? rel0 + 3 : (nz[2] ? rel0 + 2 : (nz[1] ? rel0 + 1 : (nz[0] ? rel0 : -1)));
+  r.lng = (bad || r.len > 64u) ? 1u : 0u;
+  return r;
+}
+
 // Prepend the run code of the chunk's first nonzero once the last nonzero
 // before the chunk (prev, tile-relative, -1 = none in this tile) is known.
 __device__ __forceinline__ void chunk_prepend(ChunkCode& r, int32_t prev) {
@@ -509,42 +567,29 @@ __device__ __forceinline__ void chunk_prepend(ChunkCode& r, int32_t prev) {
   }
 }
 
-template <int MODE, bool INT_IN, bool RCP>
-__device__ __forceinline__ void quantize_tile(const EncodeArgs& a, int32_t c, int64_t tile_base,
-                                              int wv, int lane, const uint32_t (&raw)[4][4],
-                                              ChunkCode (&cc)[4], float& dist, int32_t& nnz) {
-  const ClientQ cq = client_q<MODE, INT_IN>(a, c);
-  dist = 0.0f;
-  nnz = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-    int32_t q4[4];
-    quant_chunk<MODE, INT_IN, RCP>(cq, tile_base + rel0, a.P, raw[j], q4, dist);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
-    cc[j] = chunk_local(q4, rel0);
-  }
-}
-
 // Re-read and re-quantise one chunk (slow path: tiles with codes > 32 bits or
 // a body larger than the LDS window).
 template <int MODE, bool INT_IN, bool RCP>
 __device__ __forceinline__ void reload_chunk(const EncodeArgs& a, const ClientQ& cq, int32_t c,
-                                             int64_t e0, int32_t (&q4)[4]) {
+                                             int64_t e0, int32_t (&q4)[4], float& dist) {
   const uint32_t* xp = (const uint32_t*)a.xs[c];
   uint32_t r4[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) r4[k] = (e0 + k < a.P) ? xp[e0 + k] : 0u;
-  float dd = 0.0f;
-  quant_chunk<MODE, INT_IN, RCP>(cq, e0, a.P, r4, q4, dd);
+  quant_chunk<MODE, INT_IN, RCP>(cq, e0, a.P, r4, q4, dist);
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void put(T (&arr)[N], int j, T v) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) arr[i] = (j == i) ? v : arr[i];
 }
 
 #ifdef FC_STAMPS
 __device__ unsigned long long g_stamps[8];
 #define STAMP(i)                                               \
   do {                                                         \
-    if (tid == 0) {                                            \
+    if (lane == 0) {                                           \
       const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
       st_acc[i] += now_ - st_last;                             \
       st_last = now_;                                          \
@@ -554,190 +599,425 @@ __device__ unsigned long long g_stamps[8];
 #define STAMP(i) do {} while (0)
 #endif
 
+// Per-client encoder parameters, computed once per launch (k_client_params)
+// and read by k_encode with one scalar load per tile.
+struct alignas(64) ClientParam {
+  float step, rcp, s0, s1;   // step (x norm), 1/step (pow2 path), pre-scales
+  uint32_t k0, k1, c2, c3;   // scrambled Philox key / counter words (TF seed)
+  const uint32_t* x;         // the client's float32 (or int32) values
+  uint32_t* out;             // stream_buf + stream_off[c]
+  int64_t cap;               // stream_cap[c] (bytes)
+  int64_t pad;
+};
+
+__global__ void k_client_params(EncodeArgs a, ClientParam* cp, int need_key) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.nclients) return;
+  ClientParam p;
+  p.step = a.norms ? a.norms[c] * a.step : a.step;
+  p.rcp = a.rcp;
+  p.s0 = a.prescale ? a.prescale[2 * c] : 1.0f;
+  p.s1 = a.prescale ? a.prescale[2 * c + 1] : 1.0f;
+  Key4 k{0, 0, 0, 0};
+  if (need_key) k = tf_seed_scramble(a.seeds[2 * c], a.seeds[2 * c + 1]);
+  p.k0 = k.k0;
+  p.k1 = k.k1;
+  p.c2 = k.c2;
+  p.c3 = k.c3;
+  p.x = (const uint32_t*)a.xs[c];
+  p.out = (uint32_t*)(a.stream_buf + a.stream_off[c]);
+  p.cap = a.stream_cap[c];
+  p.pad = 0;
+  cp[c] = p;
+}
+
+typedef const __attribute__((address_space(4))) ClientParam* ConstParamPtr;
+
+// Field-wise read through the constant address space: one s_load per tile.
+__device__ __forceinline__ ClientParam ld_param(ConstParamPtr p) {
+  ClientParam r;
+  r.step = p->step;
+  r.rcp = p->rcp;
+  r.s0 = p->s0;
+  r.s1 = p->s1;
+  r.k0 = p->k0;
+  r.k1 = p->k1;
+  r.c2 = p->c2;
+  r.c3 = p->c3;
+  r.x = p->x;
+  r.out = p->out;
+  r.cap = p->cap;
+  r.pad = 0;
+  return r;
+}
+
+__device__ __forceinline__ ClientQ client_q_of(const ClientParam& p, bool pre) {
+  ClientQ r;
+  r.step = p.step;
+  r.rcp = p.rcp;
+  r.s0 = p.s0;
+  r.s1 = p.s1;
+  r.pre = pre;
+  r.key = Key4{p.k0, p.k1, p.c2, p.c3};
+  return r;
+}
+
+// Window layout: body bit b of the current tile lives at window bit kPre + b;
+// the tile's leading pieces (previous tile's partial word, first run code) are
+// placed just before it once the look-back has resolved them.
+constexpr uint32_t kPre = 96;
+
+// OR a code of len <= 64 bits (right-aligned in acc) into the window at bit
+// position wp: three unconditional ds_or_b32 (zero pieces are harmless);
+// positions past the window land in the guard words (the tile then takes the
+// slow path anyway).
+__device__ __forceinline__ void emit64(uint32_t* win, uint64_t acc, uint32_t len, uint32_t wp) {
+  const uint64_t X = acc << ((64u - len) & 63u);  // MSB-aligned (len 0: acc is 0)
+  const uint32_t o = wp & 31u;
+  const uint32_t i0 = min(wp >> 5, (uint32_t)kWinWords);
+  const uint32_t hi = (uint32_t)(X >> 32), lo = (uint32_t)X;
+  atomicOr(&win[i0], hi >> o);
+  atomicOr(&win[i0 + 1], __builtin_amdgcn_alignbit(hi, lo, o));
+  atomicOr(&win[i0 + 2], __builtin_amdgcn_alignbit(lo, 0u, o));
+}
+
+// 32 window bits starting at window bit s (any s; reads words s>>5, +1).
+__device__ __forceinline__ uint32_t win_bits32(const uint32_t* win, uint32_t s) {
+  const uint32_t w = s >> 5, o = s & 31u;
+  const uint64_t pair = ((uint64_t)win[w] << 32) | win[w + 1];
+  return (uint32_t)(pair >> (32u - o));
+}
+
+// Four interleaved inclusive DPP scans (independent chains hide the DPP hazard).
+__device__ __forceinline__ void dpp_incl_max4(int32_t (&x)[4]) {
+  const int32_t id = (int32_t)0x80000000;
+#define FC_MAXSTEP(ctl, rm)                                                                  \
+  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                             \
+      x[j] = max(x[j], __builtin_amdgcn_update_dpp(id, x[j], ctl, rm, 0xf, false));
+  FC_MAXSTEP(0x111, 0xf)
+  FC_MAXSTEP(0x112, 0xf)
+  FC_MAXSTEP(0x114, 0xf)
+  FC_MAXSTEP(0x118, 0xf)
+  FC_MAXSTEP(0x142, 0xa)
+  FC_MAXSTEP(0x143, 0xc)
+#undef FC_MAXSTEP
+}
+__device__ __forceinline__ void dpp_incl_sum2(uint32_t (&x)[2]) {
+#define FC_SUMSTEP(ctl, rm)                                                                  \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j)                                             \
+      x[j] += __builtin_amdgcn_update_dpp(0u, x[j], ctl, rm, 0xf, false);
+  FC_SUMSTEP(0x111, 0xf)
+  FC_SUMSTEP(0x112, 0xf)
+  FC_SUMSTEP(0x114, 0xf)
+  FC_SUMSTEP(0x118, 0xf)
+  FC_SUMSTEP(0x142, 0xa)
+  FC_SUMSTEP(0x143, 0xc)
+#undef FC_SUMSTEP
+}
+
+// Exact path (clients with a rare tile: a code past the fast path's limits or
+// a body larger than the LDS window), run by k_encode_exact after k_encode so
+// its registers do not weigh on the fast kernel.  slow_scan recomputes the tile exactly (TF cast semantics, codes of any
+// length): chunk predecessors and offsets, counts, distortion and the body's
+// last 32 bits.  slow_emit re-quantises again and emits stream-relative in
+// window passes.
+struct SlowScan {
+  int32_t chunk_prev[kChunks];
+  uint32_t chunk_off[kChunks];
+  uint32_t body;
+  int32_t carry, wfirst;
+  float dist;
+  int32_t nnz;
+  uint32_t tail;
+};
+
 template <int MODE, bool INT_IN, bool RCP>
-__global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
-  __shared__ EncShared sh;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = tid >> 6;
+__device__ __forceinline__ void slow_scan(const EncodeArgs& a, const ClientQ& cq, int32_t c,
+                                                    int64_t tile_base, uint32_t* win, uint32_t* tailw,
+                                                    SlowScan& o) {
+  const int lane = threadIdx.x;
+  for (int i = lane; i < kWinWords; i += kEncThreads) win[i] = 0;
+  int32_t carry = -1, wfirst = 0x7FFFFFFF, nnz = 0;
+  uint32_t body = 0;
+  float dist = 0.0f;
+  int32_t chunk_prev[kChunks] = {-1, -1, -1, -1};
+  uint32_t chunk_off[kChunks] = {0, 0, 0, 0};
+#pragma unroll 1
+  for (int j = 0; j < kChunks; ++j) {
+    const int32_t rel0 = 256 * j + 4 * lane;
+    int32_t q4[4];
+    reload_chunk<MODE, INT_IN, RCP>(a, cq, c, tile_base + rel0, q4, dist);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
+    ChunkCode cj = chunk_local(q4, rel0);
+    wfirst = min(wfirst, cj.first >= 0 ? cj.first : 0x7FFFFFFF);
+    const int32_t imax = dpp_incl_max(cj.last);
+    const int32_t prev = max(dpp_shr1(imax, -1), carry);
+    carry = max(carry, lane63(imax));
+    chunk_prepend(cj, prev);
+    const uint32_t isum = dpp_incl_sum(cj.len);
+    put(chunk_prev, j, prev);
+    put(chunk_off, j, body + isum - cj.len);
+    body += (uint32_t)lane63((int32_t)isum);
+  }
+  if (lane == 0) *tailw = 0;
+#pragma unroll 1
+  for (int j = 0; j < kChunks; ++j) {
+    const int32_t rel0 = 256 * j + 4 * lane;
+    int32_t qv[4];
+    float dd = 0.0f;
+    reload_chunk<MODE, INT_IN, RCP>(a, cq, c, tile_base + rel0, qv, dd);
+    int32_t prev = pick(chunk_prev, j);
+    uint32_t pos = pick(chunk_off, j);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int32_t v = qv[k];
+      if (v == 0) continue;
+      if (prev >= 0) {
+        const uint32_t d = (uint32_t)(rel0 + k - prev);
+        const uint32_t rl = glen(d);
+        pos += rl;
+        tail_emit(tailw, d, rl, pos, body);
+      }
+      const uint32_t m = mag_u32(v);
+      const uint32_t ml = glen(m);
+      const uint64_t sm = ((uint64_t)(v > 0) << ml) | m;
+      pos += 1 + ml;
+      tail_emit(tailw, sm, 1 + ml, pos, body);
+      prev = rel0 + k;
+    }
+  }
+  for (int j = 0; j < kChunks; ++j) {
+    o.chunk_prev[j] = chunk_prev[j];
+    o.chunk_off[j] = chunk_off[j];
+  }
+  o.body = body;
+  o.carry = carry;
+  o.wfirst = wfirst;
+  o.dist = dist;
+  o.nnz = nnz;
+  o.tail = uniform(*tailw);
+}
+
+struct SlowEmit {
+  uint32_t r0, tb, R0, dfirst, bstart, body, trail_len, nwords_owned, nwin_bits;
+  int32_t tile_last;
+  uint64_t trail, w0;
+  uint32_t* out32;
+  int64_t cap;
+};
+
+template <int MODE, bool INT_IN, bool RCP>
+__device__ __forceinline__ void slow_emit(const EncodeArgs& a, const ClientQ& cq, int32_t c,
+                                                    int64_t tile_base, uint32_t* win, const SlowScan& sc,
+                                                    const SlowEmit& e) {
+  const int lane = threadIdx.x;
+  const uint32_t npass = (e.nwords_owned + kWinWords - 1) / kWinWords;
+  for (uint32_t pass = 0; pass < npass; ++pass) {
+    const uint32_t plo = pass * kWinWords;
+    if (lane == 0) {
+      if (e.r0) win_emit32(win, e.tb, e.r0, 0, plo);
+      if (e.tile_last >= 0) win_emit(win, e.dfirst, e.R0, e.r0, plo);
+      if (e.trail_len) win_emit(win, e.trail, e.trail_len, e.bstart + e.body, plo);
+    }
+#pragma unroll 1
+    for (int j = 0; j < kChunks; ++j) {
+      const int32_t rel0 = 256 * j + 4 * lane;
+      int32_t prev = sc.chunk_prev[j];
+      uint32_t pos = e.bstart + sc.chunk_off[j];
+      int32_t q4[4];
+      float dd = 0.0f;
+      reload_chunk<MODE, INT_IN, RCP>(a, cq, c, tile_base + rel0, q4, dd);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int32_t v = q4[k];
+        if (v == 0) continue;
+        const uint32_t m = mag_u32(v);
+        const uint32_t ml = glen(m);
+        const uint64_t sm = ((uint64_t)(v > 0) << ml) | m;
+        if (prev >= 0) {
+          const uint32_t d = (uint32_t)(rel0 + k - prev);
+          const uint32_t rl = glen(d);
+          win_emit32(win, d, rl, pos, plo);
+          pos += rl;
+        }
+        win_emit(win, sm, 1 + ml, pos, plo);
+        pos += 1 + ml;
+        prev = rel0 + k;
+      }
+    }
+    const uint32_t nw = min((uint32_t)kWinWords, e.nwords_owned - plo);
+    for (uint32_t i = lane; i < nw; i += kEncThreads) {
+      const uint64_t wi = e.w0 + plo + i;
+      if ((int64_t)(wi + 1) * 4 <= e.cap) e.out32[wi] = bswap32(win[i]);
+    }
+    const uint32_t nt = min((uint32_t)kWinWords, (e.nwin_bits + 31) / 32 - plo);
+    for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
+  }
+}
+
+// One wavefront = one workgroup = one 1024-element tile at a time: no barriers,
+// every cross-lane step is DPP / ballot / readlane, the bit window is the
+// wave's own LDS; independent waves hide each other's latencies.
+template <int MODE, bool INT_IN, bool RCP>
+__global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs a) {
+  __shared__ uint32_t win[kWinWords + 3];  // + guard words for out-of-window emission
+  __shared__ uint32_t tailw;
+  const int lane = threadIdx.x;
   const uint32_t total_tiles = (uint32_t)a.nclients * (uint32_t)a.T;
+  const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
+  const bool pre = !INT_IN && a.prescale != nullptr;
 #ifdef FC_STAMPS
   uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
-
-  for (int i = tid; i < kWinWords; i += kThreads) sh.win[i] = 0;
-  if (tid == 0) sh.ticket = atomicAdd(a.counter, 1u);
-  __syncthreads();
-  uint32_t ticket = sh.ticket;
-  uint32_t raw[4][4];
-  if (ticket < total_tiles) load_raw<INT_IN>(a, ticket, wv, lane, raw);
+  for (int i = lane; i < kWinWords + 3; i += kEncThreads) win[i] = 0;
+  const uint32_t shard = blockIdx.x % a.nshards;
+  uint32_t* my_counter = a.counter + kShardStride * shard;
+  uint32_t tk = 0;
+  if (lane == 0) tk = atomicAdd(my_counter, 1u);
+  uint32_t ticket = shard + a.nshards * uniform(tk);
 
   while (ticket < total_tiles) {
     STAMP(0);
-    if (tid == 0) {
-      sh.next_ticket = atomicAdd(a.counter, 1u);  // read after the first barrier
-      sh.tail = 0;
-      sh.slow = 0;
-    }
-    // tickets interleave clients (tile-major) so each client has few tiles in
-    // flight and the look-back almost always finds a prefix at distance 1
+    // tickets interleave clients (tile-major) so each client has few tiles in flight
     const int32_t t = (int32_t)(ticket / (uint32_t)a.nclients);
     const int32_t c = (int32_t)(ticket - (uint32_t)t * (uint32_t)a.nclients);
     const int64_t P = a.P;
     const int64_t tile_base = (int64_t)t * kTE;
     const bool last_tile = (t == a.T - 1);
+    const bool full = tile_base + kTE <= P;
+    const ClientParam cp = ld_param(cparams + c);
+    // raw values: chunk j of this lane = tile elements [256 j + 4 lane, +4)
+    uint32_t raw[kChunks][4];
+#pragma unroll
+    for (int j = 0; j < kChunks; ++j) {
+      const int64_t e0 = tile_base + 256 * j + 4 * lane;
+      if (full) {
+        const uint4 v = *(const uint4*)(cp.x + e0);
+        raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) raw[j][k] = (e0 + k < P) ? cp.x[e0 + k] : 0u;
+      }
+    }
+    uint32_t ntk = 0;
+    if (lane == 0) ntk = atomicAdd(my_counter, 1u);  // next ticket, used after phase D
+    // predecessor's status, fetched now so that the common case (its inclusive
+    // prefix is already published) costs no round trip at the look-back
+    uint64_t pw1 = 0, pw2 = 0;
+    if (t > 0) {
+      const uint64_t* sp = a.status + 2 * ((int64_t)c * a.T + t - 1);
+      pw1 = ld_agent(sp);
+      pw2 = ld_agent(sp + 1);
+    }
 
-    // ---- phase A: quantise + chunk-local codes (4 chunks of 4 consecutive elements) ----
-    ChunkCode cc[4];
-    float dist;
-    int32_t nnz;
-    quantize_tile<MODE, INT_IN, RCP>(a, c, tile_base, wv, lane, raw, cc, dist, nnz);
+    // ---- A: quantise + chunk-local codes ----
+    ChunkCode cc[kChunks];
+    float dist = 0.0f;
+    int32_t nnz = 0;
+    {
+      const ClientQ cq = client_q_of(cp, pre);
+#pragma unroll
+      for (int j = 0; j < kChunks; ++j) {
+        const int32_t rel0 = 256 * j + 4 * lane;
+        if (INT_IN || (FC_ABL & 8)) {
+          int32_t q4[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) q4[k] = (FC_ABL & 8) ? (int32_t)(raw[j][k] >> 29) - 3 : (int32_t)raw[j][k];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
+          cc[j] = chunk_local(q4, rel0);
+        } else {
+          const uint32_t g = (uint32_t)((tile_base + rel0) >> 2);
+          if (MODE == FC_DITHERED && !full)
+            cc[j] = quant_code_fast<MODE, RCP, true>(cq, g, raw[j], rel0, dist, nnz,
+                                                     (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - rel0)));
+          else
+            cc[j] = quant_code_fast<MODE, RCP>(cq, g, raw[j], rel0, dist, nnz);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one chunk at a time: bounded mask/VGPR pressure
+      }
+    }
     STAMP(1);
 
-    // ---- phase B: wave max-scan of the chunks' last nonzero ----
-    int32_t chunk_prev[4];  // last nonzero before the chunk (tile-relative), or -1
+    // ---- B: last nonzero before each chunk (4 interleaved max-scans over
+    //      (chunk, lane) order), then the chunks' run-code prepends ----
     int32_t carry = -1, wfirst = 0x7FFFFFFF;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      wfirst = min(wfirst, cc[j].first >= 0 ? cc[j].first : 0x7FFFFFFF);
-      const int32_t incl = dpp_incl_max(cc[j].last);
-      chunk_prev[j] = max(dpp_shr1(incl, -1), carry);
-      carry = max(carry, lane63(incl));
-    }
+    uint32_t lng = 0;
     {
-      float d = dist;
-      int32_t n = nnz;
-      int32_t f = wfirst;
+      int32_t im[kChunks];
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        d += __shfl_xor(d, o, 64);
-        n += __shfl_xor(n, o, 64);
-        f = min(f, __shfl_xor(f, o, 64));
-      }
-      if (lane == 0) {
-        sh.wave_dist[wv] = d;
-        sh.wave_nnz[wv] = n;
-        sh.wave_last[wv] = carry;
-        sh.wave_first[wv] = f;
+      for (int j = 0; j < kChunks; ++j) im[j] = cc[j].last;
+      dpp_incl_max4(im);
+#pragma unroll
+      for (int j = 0; j < kChunks; ++j) {
+        const int32_t prev = max(dpp_shr1(im[j], -1), carry);
+        carry = max(carry, lane63(im[j]));
+        wfirst = min(wfirst, cc[j].first >= 0 ? cc[j].first : 0x7FFFFFFF);
+        chunk_prepend(cc[j], prev);
+        lng |= cc[j].lng;
       }
     }
-    __syncthreads();
-    STAMP(2);
-    int32_t wave_in = -1;
-    for (int w = 0; w < wv; ++w) wave_in = max(wave_in, sh.wave_last[w]);
-    int32_t tile_first = 0x7FFFFFFF, tile_last = -1;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      tile_first = min(tile_first, sh.wave_first[w]);
-      tile_last = max(tile_last, sh.wave_last[w]);
+    // ---- C: body-relative offsets (two packed 16-bit sum-scans) ----
+    uint32_t off[kChunks];
+    uint32_t body;
+    {
+      uint32_t s2[2] = {cc[0].len | (cc[1].len << 16), cc[2].len | (cc[3].len << 16)};
+      dpp_incl_sum2(s2);
+      const uint32_t t0 = (uint32_t)lane63((int32_t)s2[0]), t1 = (uint32_t)lane63((int32_t)s2[1]);
+      const uint32_t b1 = t0 & 0xFFFFu, b2 = b1 + (t0 >> 16), b3 = b2 + (t1 & 0xFFFFu);
+      off[0] = (s2[0] & 0xFFFFu) - cc[0].len;
+      off[1] = b1 + (s2[0] >> 16) - cc[1].len;
+      off[2] = b2 + (s2[1] & 0xFFFFu) - cc[2].len;
+      off[3] = b3 + (s2[1] >> 16) - cc[3].len;
+      body = b3 + (t1 >> 16);
     }
-    if (tid == 0) {
-      const float d = ((sh.wave_dist[0] + sh.wave_dist[1]) + sh.wave_dist[2]) + sh.wave_dist[3];
-      const int32_t n = sh.wave_nnz[0] + sh.wave_nnz[1] + sh.wave_nnz[2] + sh.wave_nnz[3];
-      if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
-      if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t] = n;
-    }
-    const uint32_t next = sh.next_ticket;
-
-    // ---- phase C: complete the chunk codes, sum-scan of their lengths ----
-    uint64_t cacc[4];
-    uint32_t chunk_off[4], clen[4];
-    uint32_t wbits = 0, lng = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      chunk_prev[j] = max(chunk_prev[j], wave_in);
-      chunk_prepend(cc[j], chunk_prev[j]);
-      cacc[j] = cc[j].acc;
-      clen[j] = cc[j].len;
-      lng |= cc[j].lng;
-      const uint32_t incl = dpp_incl_sum(cc[j].len);
-      chunk_off[j] = wbits + incl - cc[j].len;
-      wbits += (uint32_t)lane63((int32_t)incl);
-    }
-    if (lane == 0) sh.wave_bits[wv] = wbits;
-    if (lng) sh.slow = 1;
-    __syncthreads();
-    STAMP(3);
-    uint32_t woff = 0, body = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      woff += (w < wv) ? sh.wave_bits[w] : 0u;
-      body += sh.wave_bits[w];
-    }
-    // fast path: no code > 32 bits and the body (+ trailing code + one funnel
-    // word) fits the LDS window
-    const bool fast = !sh.slow && body + 64u <= 32u * (kWinWords - 1);
-
-    // ---- phase D: emit the body at body-relative bit offsets (fast path), or
-    //      compute just its last 32 bits (slow path); prefetch the next tile ----
-    if (fast) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (clen[j]) win_emit(sh.win, cacc[j], clen[j], woff + chunk_off[j], 0);
+    // fast path: whole tile inside the tensor (or int input), no long chunk, and
+    // prefix + body + trailing code + one funnel word fit the wave's window
+    const bool fast = __ballot(lng != 0) == 0 && kPre + body + 96u <= 32u * kWinWords;
+    // ---- D: emit (body-relative) ----
+    if (FC_ABL & 1) {
+      asm volatile("" :: "v"((uint32_t)cc[0].acc), "v"((uint32_t)cc[3].acc), "v"(off[0]), "v"(off[3]));
     } else {
-      // slow tile: recompute codes element by element (any length) for the tail
-      const ClientQ cq = client_q<MODE, INT_IN>(a, c);
-#pragma unroll 1
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t off = woff + (j == 0 ? chunk_off[0] : j == 1 ? chunk_off[1] : j == 2 ? chunk_off[2] : chunk_off[3]);
-        const uint32_t cl = (j == 0 ? clen[0] : j == 1 ? clen[1] : j == 2 ? clen[2] : clen[3]);
-        if (off + cl + 32 < body || cl == 0) continue;
-        const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-        int32_t qv[4];
-        reload_chunk<MODE, INT_IN, RCP>(a, cq, c, tile_base + rel0, qv);
-        int32_t prev = (j == 0 ? chunk_prev[0] : j == 1 ? chunk_prev[1] : j == 2 ? chunk_prev[2] : chunk_prev[3]);
-        uint32_t pos = off;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int32_t v = qv[k];
-          if (v == 0) continue;
-          if (prev >= 0) {
-            const uint32_t d = (uint32_t)(rel0 + k - prev);
-            const uint32_t rl = glen(d);
-            pos += rl;
-            tail_emit(&sh.tail, d, rl, pos, body);
-          }
-          const uint32_t m = mag_u32(v);
-          const uint32_t ml = glen(m);
-          const uint64_t sm = ((uint64_t)(v > 0) << ml) | m;
-          pos += 1 + ml;
-          tail_emit(&sh.tail, sm, 1 + ml, pos, body);
-          prev = rel0 + k;
-        }
+      for (int j = 0; j < kChunks; ++j) emit64(win, cc[j].acc, cc[j].len, kPre + off[j]);
+    }
+    STAMP(2);
+
+    const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;  // body's last 32 bits
+    const int32_t tile_last = carry;
+    const int32_t tile_first = wave_min_i(wfirst);
+    if (fast) {
+      const float d = wave_sum_f(dist);
+      const int32_t n = wave_sum_i(nnz);
+      if (lane == 0) {
+        if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
+        if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t] = n;
       }
     }
-    if (next < total_tiles) load_raw<INT_IN>(a, next, wv, lane, raw);
-    __syncthreads();
-    STAMP(4);
+    const uint32_t next = shard + a.nshards * uniform(ntk);
+    STAMP(3);
 
-    // ---- phase E: publish aggregate, decoupled look-back (wave 0) ----
-    if (wv == 0) {
-      uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t);
-      Seg agg;
-      agg.has_nz = tile_last >= 0;
-      agg.first = agg.has_nz ? (int32_t)(tile_base + tile_first) : 0;
-      agg.last = agg.has_nz ? (int32_t)(tile_base + tile_last) : 0;
-      agg.body = body;
-      if (fast) {
-        uint32_t tl = 0;
-        if (body >= 32) {
-          const uint32_t s = body - 32, w = s >> 5, o = s & 31;
-          tl = o ? (sh.win[w] << o) | (sh.win[w + 1] >> (32 - o)) : sh.win[w];
-        } else if (body) {
-          tl = sh.win[0] >> (32 - body);
-        }
-        agg.tail = tl;
-      } else {
-        agg.tail = sh.tail;
-      }
-      Seg excl;
+    // ---- E: decoupled look-back ----
+    uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t);
+    Seg agg;
+    agg.has_nz = tile_last >= 0;
+    agg.first = agg.has_nz ? (int32_t)(tile_base + tile_first) : 0;
+    agg.last = agg.has_nz ? (int32_t)(tile_base + tile_last) : 0;
+    agg.body = body;
+    agg.tail = agg_tail;
+    bool slow = !fast;
+    Seg excl = seg_identity();
+    if (!slow) {
       if (t == 0) {
         excl.has_nz = 1;
         excl.first = -1;
         excl.last = -1;
-        excl.body = 0;
-        excl.tail = 0;
+      } else if ((pw1 >> 62) == 2 && (pw2 >> 62) == 2) {
+        excl = seg_from_status(pw1, pw2, 0);  // predecessor's inclusive prefix
+      } else if ((pw1 >> 62) == 3 && (pw2 >> 62) == 3) {
+        slow = true;  // predecessor left to the exact kernel
       } else {
         if (lane == 0) {
           const uint64_t fr = agg.has_nz ? (uint64_t)tile_first : kNoPos;
@@ -745,133 +1025,193 @@ __global__ __launch_bounds__(kThreads, 4) void k_encode(EncodeArgs a) {
           st_agent(st + 1, kFlagAgg | agg.tail);
           st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
         }
-        excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, a.spin_err);
-      }
-      const Seg incl = seg_combine(excl, agg);
-      if (lane == 0) {
-        st_agent(st + 1, kFlagPre | incl.tail);
-        st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
-        const int64_t ib = (int64_t)c * (a.T + 1);
-        a.idx[ib + t] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
-        sh.b0 = excl.body;
-        sh.last_before = excl.last;
-        sh.tail_before = excl.tail;
-        const uint32_t r0 = (uint32_t)(excl.body & 31);
-        uint32_t R0 = 0;
-        if (agg.has_nz) R0 = glen((uint32_t)(agg.first - excl.last));
-        sh.r0_R0 = r0 + R0;
-        uint32_t tl = 0;
-        uint64_t tv = 0;
-        if (last_tile) {
-          const int64_t zc = P - 1 - (int64_t)incl.last;  // trailing zeros
-          if (zc > 0) {
-            tv = (uint64_t)(zc + 1);
-            tl = 2u * (63u - (uint32_t)__clzll(tv)) + 1u;
-            if (fast) win_emit(sh.win, tv, tl, body, 0);  // body-relative
-          }
-          a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
-          a.total_bits[c] = (int64_t)incl.body + tl;
-        }
-        sh.trail = tv;
-        sh.trail_len = tl;
-        sh.nwin_bits = r0 + R0 + body + tl;
-      }
-    }
-    __syncthreads();
-    STAMP(5);
-
-    // ---- phase F: store the words this tile owns ----
-    const uint64_t b0 = sh.b0;
-    const uint32_t bstart = sh.r0_R0;
-    const uint32_t nwin_bits = sh.nwin_bits;
-    const int32_t last_before = sh.last_before;
-    const uint32_t nwords_owned = last_tile ? (nwin_bits + 31) / 32 : nwin_bits / 32;
-    const int64_t cap = a.stream_cap[c];
-    uint32_t* out32 = (uint32_t*)(a.stream_buf + a.stream_off[c]);
-    const uint64_t w0 = b0 >> 5;
-    const uint32_t r0 = (uint32_t)(b0 & 31);
-    if (tid == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&a.overflow[c], 1u);
-    if (fast) {
-      const uint32_t dfirst = tile_last >= 0 ? (uint32_t)(tile_base + tile_first - last_before) : 0u;
-      const uint32_t R0 = bstart - r0;
-      const uint32_t tb = sh.tail_before & (r0 ? ((1u << r0) - 1u) : 0u);
-      for (uint32_t k = tid; k < nwords_owned; k += kThreads) {
-        // stream-window bits [32k, 32k+32) = body bits [32k - bstart, ...)
-        const int32_t s = 32 * (int32_t)k - (int32_t)bstart;
-        uint32_t wv32;
-        if (s >= 0) {
-          const uint32_t w = (uint32_t)s >> 5, o = (uint32_t)s & 31;
-          wv32 = o ? (sh.win[w] << o) | (sh.win[w + 1] >> (32 - o)) : sh.win[w];
+        if (FC_ABL & 4) {
+          excl.has_nz = 1;
+          excl.first = excl.last = -1;
         } else {
-          wv32 = (-s < 32) ? (sh.win[0] >> -s) : 0u;
-          wv32 |= piece_word(tb, r0, 0, k) | piece_word(dfirst, R0, r0, k);
+          excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, a.spin_err, slow);
         }
-        if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
-      }
-      __syncthreads();
-      const uint32_t nt = min((uint32_t)kWinWords, (body + sh.trail_len + 31) / 32 + 1);
-      for (uint32_t i = tid; i < nt; i += kThreads) sh.win[i] = 0;
-    } else {
-      // slow path (a code > 32 bits, or a body larger than the LDS window):
-      // re-read and re-quantise this tile one chunk at a time and emit
-      // stream-relative in window passes
-      const ClientQ cq = client_q<MODE, INT_IN>(a, c);
-      const uint32_t npass = (nwords_owned + kWinWords - 1) / kWinWords;
-      for (uint32_t pass = 0; pass < npass; ++pass) {
-        const uint32_t plo = pass * kWinWords;
-        if (tid == 0) {
-          if (r0) win_emit32(sh.win, sh.tail_before & ((1u << r0) - 1u), r0, 0, plo);
-          if (tile_last >= 0) {
-            const uint32_t d = (uint32_t)(tile_base + tile_first - last_before);
-            win_emit(sh.win, d, glen(d), r0, plo);
-          }
-          if (sh.trail_len) win_emit(sh.win, sh.trail, sh.trail_len, bstart + body, plo);
-        }
-#pragma unroll 1
-        for (int j = 0; j < 4; ++j) {
-          const int32_t rel0 = 1024 * wv + 256 * j + 4 * lane;
-          int32_t prev = j == 0 ? chunk_prev[0] : j == 1 ? chunk_prev[1] : j == 2 ? chunk_prev[2] : chunk_prev[3];
-          uint32_t pos = bstart + woff +
-                         (j == 0 ? chunk_off[0] : j == 1 ? chunk_off[1] : j == 2 ? chunk_off[2] : chunk_off[3]);
-          int32_t q4[4];
-          reload_chunk<MODE, INT_IN, RCP>(a, cq, c, tile_base + rel0, q4);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int32_t v = q4[k];
-            if (v == 0) continue;
-            const uint32_t m = mag_u32(v);
-            const uint32_t ml = glen(m);
-            const uint64_t sm = ((uint64_t)(v > 0) << ml) | m;
-            if (prev >= 0) {
-              const uint32_t d = (uint32_t)(rel0 + k - prev);
-              const uint32_t rl = glen(d);
-              win_emit32(sh.win, d, rl, pos, plo);
-              pos += rl;
-            }
-            win_emit(sh.win, sm, 1 + ml, pos, plo);
-            pos += 1 + ml;
-            prev = rel0 + k;
-          }
-        }
-        __syncthreads();
-        const uint32_t nw = min((uint32_t)kWinWords, nwords_owned - plo);
-        for (uint32_t i = tid; i < nw; i += kThreads) {
-          const uint64_t wi = w0 + plo + i;
-          if ((int64_t)(wi + 1) * 4 <= cap) out32[wi] = bswap32(sh.win[i]);
-        }
-        __syncthreads();
-        const uint32_t nt = min((uint32_t)kWinWords, (nwin_bits + 31) / 32 - plo);
-        for (uint32_t i = tid; i < nt; i += kThreads) sh.win[i] = 0;
-        __syncthreads();
       }
     }
-    STAMP(6);
+    if (slow) {
+      // this tile (a long code or a body beyond the window), or one before it, is
+      // re-encoded by k_encode_exact together with the rest of the client
+      if (lane == 0) {
+        st_agent(st + 1, kFlagSlow);
+        st_agent(st, kFlagSlow);
+        if (atomicOr(&a.slow_flag[c], 1) == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = c;
+      }
+      for (int i = lane; i < kWinWords; i += kEncThreads) win[i] = 0;
+      ticket = next;
+      continue;
+    }
+    const Seg incl = seg_combine(excl, agg);
+    const uint32_t r0 = (uint32_t)(excl.body & 31);
+    const uint32_t dfirst = agg.has_nz ? (uint32_t)(agg.first - excl.last) : 0u;
+    const uint32_t R0 = agg.has_nz ? glen(dfirst) : 0u;
+    const uint32_t bstart = r0 + R0;  // stream-window bit where the body starts
+    const uint32_t tb = excl.tail & (r0 ? ((1u << r0) - 1u) : 0u);
+    uint32_t trail_len = 0;
+    uint64_t trail = 0;
+    if (last_tile) {
+      const int64_t zc = P - 1 - (int64_t)incl.last;  // trailing zeros
+      if (zc > 0) {
+        trail = (uint64_t)(zc + 1);
+        trail_len = 2u * (63u - (uint32_t)__clzll(trail)) + 1u;
+      }
+    }
+    if (lane == 0) {
+      st_agent(st + 1, kFlagPre | incl.tail);
+      st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+      const int64_t ib = (int64_t)c * (a.T + 1);
+      a.idx[ib + t] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
+      if (last_tile) {
+        a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
+        a.total_bits[c] = (int64_t)incl.body + trail_len;
+      }
+      // leading pieces just before the body, trailing code after it
+      emit64(win, tb, r0, kPre - bstart);
+      emit64(win, dfirst, R0, kPre - R0);
+      if (trail_len) emit64(win, trail, trail_len, kPre + body);
+    }
+    STAMP(4);
+
+    // ---- F: store the words this tile owns ----
+    const uint32_t nwin_bits = bstart + body + trail_len;
+    const uint32_t nwords_owned = last_tile ? (nwin_bits + 31) / 32 : nwin_bits / 32;
+    const int64_t cap = cp.cap;
+    uint32_t* out32 = cp.out;
+    const uint64_t w0 = excl.body >> 5;
+    if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&a.overflow[c], 1u);
+    const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
+    for (uint32_t k = lane; k < nwords_owned; k += kEncThreads) {
+      const uint32_t wv32 = win_bits32(win, s0 + 32 * k);
+      if (FC_ABL & 2) asm volatile("" :: "v"(wv32));
+      else if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
+    }
+    const uint32_t nt = min((uint32_t)kWinWords, (kPre + body + trail_len + 31) / 32 + 1);
+    for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
+    STAMP(5);
     ticket = next;
   }
 #ifdef FC_STAMPS
-  if (tid == 0)
+  if (lane == 0)
     for (int i = 0; i < 8; ++i) atomicAdd(&g_stamps[i], (unsigned long long)st_acc[i]);
 #endif
+}
+
+// Reset the look-back status (and overflow flag) of the clients k_encode
+// handed over, so k_encode_exact can chain them afresh.
+__global__ void k_zero_slow(EncodeArgs a) {
+  const uint32_t n = *a.slow_count;
+  const int64_t per = 2 * (int64_t)a.T;
+  const int64_t total = (int64_t)n * per;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = i / per;
+    const int32_t c = a.slow_list[l];
+    a.status[(int64_t)c * per + (i - l * per)] = 0;
+    if (i - l * per == 0) a.overflow[c] = 0;
+  }
+}
+
+// Exact re-encode of the handed-over clients: every tile requantised with TF
+// cast semantics, codes of any length, emitted stream-relative in window
+// passes; same decoupled look-back (tile-major tickets over those clients).
+template <int MODE, bool INT_IN, bool RCP>
+__global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
+  __shared__ uint32_t win[kWinWords + 3];
+  __shared__ uint32_t tailw;
+  const int lane = threadIdx.x;
+  const uint32_t n = *a.slow_count;
+  if (n == 0) return;
+  const uint32_t total_tiles = n * (uint32_t)a.T;
+  const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
+  const bool pre = !INT_IN && a.prescale != nullptr;
+  for (int i = lane; i < kWinWords + 3; i += kEncThreads) win[i] = 0;
+  for (;;) {
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter2, 1u);
+    const uint32_t ticket = uniform(tk);
+    if (ticket >= total_tiles) break;
+    const int32_t t = (int32_t)(ticket / n);
+    const int32_t c = a.slow_list[ticket - (uint32_t)t * n];
+    const int64_t P = a.P;
+    const int64_t tile_base = (int64_t)t * kTE;
+    const bool last_tile = (t == a.T - 1);
+    const ClientParam cp = ld_param(cparams + c);
+    const ClientQ cq = client_q_of(cp, pre);
+    SlowScan sc;
+    slow_scan<MODE, INT_IN, RCP>(a, cq, c, tile_base, win, &tailw, sc);
+    const int32_t tile_last = sc.carry;
+    const int32_t tile_first = wave_min_i(sc.wfirst);
+    const uint32_t body = sc.body;
+    {
+      const float d = wave_sum_f(sc.dist);
+      const int32_t nz = wave_sum_i(sc.nnz);
+      if (lane == 0) {
+        if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
+        if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t] = nz;
+      }
+    }
+    uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t);
+    Seg agg;
+    agg.has_nz = tile_last >= 0;
+    agg.first = agg.has_nz ? (int32_t)(tile_base + tile_first) : 0;
+    agg.last = agg.has_nz ? (int32_t)(tile_base + tile_last) : 0;
+    agg.body = body;
+    agg.tail = sc.tail;
+    Seg excl = seg_identity();
+    if (t == 0) {
+      excl.has_nz = 1;
+      excl.first = -1;
+      excl.last = -1;
+    } else {
+      if (lane == 0) {
+        const uint64_t fr = agg.has_nz ? (uint64_t)tile_first : kNoPos;
+        const uint64_t lr = agg.has_nz ? (uint64_t)tile_last : kNoPos;
+        st_agent(st + 1, kFlagAgg | agg.tail);
+        st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
+      }
+      bool slow = false;
+      excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, a.spin_err, slow);
+    }
+    const Seg incl = seg_combine(excl, agg);
+    SlowEmit e;
+    e.r0 = (uint32_t)(excl.body & 31);
+    e.dfirst = agg.has_nz ? (uint32_t)(agg.first - excl.last) : 0u;
+    e.R0 = agg.has_nz ? glen(e.dfirst) : 0u;
+    e.bstart = e.r0 + e.R0;
+    e.tb = excl.tail & (e.r0 ? ((1u << e.r0) - 1u) : 0u);
+    e.body = body;
+    e.trail_len = 0;
+    e.trail = 0;
+    if (last_tile) {
+      const int64_t zc = P - 1 - (int64_t)incl.last;
+      if (zc > 0) {
+        e.trail = (uint64_t)(zc + 1);
+        e.trail_len = 2u * (63u - (uint32_t)__clzll(e.trail)) + 1u;
+      }
+    }
+    if (lane == 0) {
+      st_agent(st + 1, kFlagPre | incl.tail);
+      st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+      const int64_t ib = (int64_t)c * (a.T + 1);
+      a.idx[ib + t] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
+      if (last_tile) {
+        a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
+        a.total_bits[c] = (int64_t)incl.body + e.trail_len;
+      }
+    }
+    e.nwin_bits = e.bstart + body + e.trail_len;
+    e.nwords_owned = last_tile ? (e.nwin_bits + 31) / 32 : e.nwin_bits / 32;
+    e.tile_last = tile_last;
+    e.w0 = excl.body >> 5;
+    e.out32 = cp.out;
+    e.cap = cp.cap;
+    if (lane == 0 && (int64_t)(e.w0 + e.nwords_owned) * 4 > e.cap) atomicOr((uint32_t*)&a.overflow[c], 1u);
+    slow_emit<MODE, INT_IN, RCP>(a, cq, c, tile_base, win, sc, e);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1264,7 +1604,20 @@ int check_launch(const char* what) {
 
 int64_t tiles_for(int64_t P) { return (P + kTE - 1) / kTE; }
 
-int64_t enc_status_bytes(int32_t n, int64_t P) { return ((int64_t)n * tiles_for(P) * 16 + 64 + 255) & ~255LL; }
+// Workspace: [status n*T*16][header: ticket shards, spin_err, counter2,
+// slow_count][slow_flag n*4] (all zeroed per launch) [slow_list n*4]
+// [ClientParam n*64].
+constexpr int kHdrWords = kShardStride * (kTicketShards + 3);
+int64_t enc_status_bytes(int32_t n, int64_t P) { return (int64_t)n * tiles_for(P) * 16; }
+int64_t enc_zeroed_bytes(int32_t n, int64_t P) {
+  return enc_status_bytes(n, P) + 4 * kHdrWords + 4 * (int64_t)n;
+}
+int64_t enc_params_offset(int32_t n, int64_t P) {
+  return (enc_zeroed_bytes(n, P) + 4 * (int64_t)n + 255) & ~255LL;
+}
+int64_t enc_workspace_bytes(int32_t n, int64_t P) {
+  return enc_params_offset(n, P) + (int64_t)n * (int64_t)sizeof(ClientParam);
+}
 
 int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step, const float* norms,
                   const float* prescale, const int64_t* seeds, int mode, bool int_in, uint8_t* stream_buf,
@@ -1284,7 +1637,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   hipStream_t s = (hipStream_t)stream;
   const int64_t T = tiles_for(P);
   const int64_t sb = enc_status_bytes(nclients, P);
-  if (hipMemsetAsync(workspace, 0, sb, s) != hipSuccess) return fail(-10, "memset status");
+  if (hipMemsetAsync(workspace, 0, enc_zeroed_bytes(nclients, P), s) != hipSuccess) return fail(-10, "memset status");
   if (hipMemsetAsync(overflow, 0, sizeof(int32_t) * nclients, s) != hipSuccess) return fail(-10, "memset overflow");
   EncodeArgs a;
   a.xs = xs;
@@ -1304,34 +1657,49 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   a.nnz_part = nnz_part;
   a.overflow = overflow;
   a.status = (uint64_t*)workspace;
-  a.counter = (uint32_t*)((uint8_t*)workspace + (int64_t)nclients * T * 16);
-  a.spin_err = a.counter + 4;
+  a.counter = (uint32_t*)((uint8_t*)workspace + sb);
+  a.spin_err = a.counter + kShardStride * kTicketShards;
+  a.counter2 = a.counter + kShardStride * (kTicketShards + 1);
+  a.slow_count = a.counter + kShardStride * (kTicketShards + 2);
+  a.slow_flag = (int32_t*)(a.counter + kHdrWords);
+  a.slow_list = a.slow_flag + nclients;
+  a.cparams = (const uint8_t*)workspace + enc_params_offset(nclients, P);
   int dev = 0, ncu = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t total = (int64_t)nclients * T;
   // few clients: cap the tiles in flight per client so look-back windows stay short
-  int64_t max_grid = std::min<int64_t>((int64_t)ncu * 8, std::max<int64_t>(128, 64LL * nclients));
-  if (const char* g = getenv("FEDCODEC_ENC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
-  const int grid = (int)std::min<int64_t>(total, max_grid);
   // power-of-two step (no per-client normalisation): x / step == x * (1 / step)
   int ex = 0;
   const bool pow2 = !int_in && !norms && std::frexp(step, &ex) == 0.5f && std::isnormal(1.0f / step);
   a.rcp = pow2 ? 1.0f / step : 0.0f;
-  const dim3 g(grid), b(kThreads);
-  if (int_in) {
-    hipLaunchKernelGGL((k_encode<FC_UNIFORM, true, false>), g, b, 0, s, a);
-  } else if (mode == FC_UNIFORM) {
-    if (pow2) hipLaunchKernelGGL((k_encode<FC_UNIFORM, false, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_encode<FC_UNIFORM, false, false>), g, b, 0, s, a);
-  } else if (mode == FC_STOCHASTIC) {
-    if (pow2) hipLaunchKernelGGL((k_encode<FC_STOCHASTIC, false, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_encode<FC_STOCHASTIC, false, false>), g, b, 0, s, a);
-  } else {
-    if (pow2) hipLaunchKernelGGL((k_encode<FC_DITHERED, false, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_encode<FC_DITHERED, false, false>), g, b, 0, s, a);
-  }
-  return check_launch("k_encode");
+  void (*kern)(EncodeArgs) = nullptr;
+  void (*exact)(EncodeArgs) = nullptr;
+#define FC_PICK(M, I, R) (kern = k_encode<M, I, R>, exact = k_encode_exact<M, I, R>)
+  if (int_in) FC_PICK(FC_UNIFORM, true, false);
+  else if (mode == FC_UNIFORM) pow2 ? FC_PICK(FC_UNIFORM, false, true) : FC_PICK(FC_UNIFORM, false, false);
+  else if (mode == FC_STOCHASTIC) pow2 ? FC_PICK(FC_STOCHASTIC, false, true) : FC_PICK(FC_STOCHASTIC, false, false);
+  else pow2 ? FC_PICK(FC_DITHERED, false, true) : FC_PICK(FC_DITHERED, false, false);
+#undef FC_PICK
+  // Persistent grid no larger than what is co-resident (every ticket stream has a
+  // running workgroup); few clients: cap the tiles in flight per client so the
+  // look-back windows stay short.
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kEncThreads, 0) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  int64_t max_grid = std::min<int64_t>((int64_t)ncu * per_cu, std::max<int64_t>(128, 64LL * nclients));
+  if (const char* g = getenv("FEDCODEC_ENC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
+  const int grid = (int)std::min<int64_t>(total, max_grid);
+  a.nshards = (uint32_t)std::min(kTicketShards, grid);
+  hipLaunchKernelGGL(k_client_params, dim3((nclients + 255) / 256), dim3(256), 0, s, a,
+                     (ClientParam*)a.cparams, (int)(!int_in && mode != FC_UNIFORM));
+  if (hipGetLastError() != hipSuccess) return fail(-10, "k_client_params launch");
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kEncThreads), 0, s, a);
+  if (hipGetLastError() != hipSuccess) return check_launch("k_encode");
+  // clients with a tile beyond the fast path: exact re-encode (no-ops otherwise)
+  hipLaunchKernelGGL(k_zero_slow, dim3(256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(exact, dim3(grid), dim3(kEncThreads), 0, s, a);
+  return check_launch("k_encode_exact");
 }
 
 }  // namespace
@@ -1353,7 +1721,7 @@ int fc_debug_stamps(unsigned long long* host8, int reset) {
 int64_t fc_num_tiles(int64_t P) { return P <= 0 ? 0 : tiles_for(P); }
 int64_t fc_encode_workspace_bytes(int32_t nclients, int64_t P) {
   if (nclients <= 0 || P <= 0) return 256;
-  return enc_status_bytes(nclients, P);
+  return enc_workspace_bytes(nclients, P);
 }
 
 int fc_quantize(const float* x, int64_t P, float step, int64_t seed0, int64_t seed1, int mode,

@@ -58,7 +58,7 @@ extern "C" {
 #define FC_NORM_L2 4   /* tf.linalg.global_norm: clipping_factory */
 #define FC_NORM_LINF 5 /* max |x|: zeroing_factory (norm_order=inf) */
 
-#define FC_TILE_ELEMS 4096       /* encoder tile = decoder index granularity */
+#define FC_TILE_ELEMS 1024       /* encoder tile (one wavefront) = decoder index granularity */
 #define FC_MAX_ELEMS 67108863LL  /* P limit: 2^26 - 1 elements per client tensor */
 
 const char* fc_last_error(void);

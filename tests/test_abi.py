@@ -33,9 +33,9 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
   lib = _lib.load()
   assert lib.fc_version().startswith(b"fedcodec")
-  assert lib.fc_num_tiles(25_000_000) == 6104
+  assert lib.fc_num_tiles(25_000_000) == 24415
   assert lib.fc_num_tiles(0) == 0
-  assert lib.fc_encode_workspace_bytes(128, 25_000_000) >= 128 * 6104 * 16
+  assert lib.fc_encode_workspace_bytes(128, 25_000_000) >= 128 * 24415 * 16
 
 
 def test_argument_validation_without_gpu():

@@ -72,7 +72,7 @@ def _rand_q(rng, P, kind):
   return q
 
 
-@pytest.mark.parametrize("P", [1, 3, 4, 5, 1023, 4096, 4099, 20000, 100003])
+@pytest.mark.parametrize("P", [1, 3, 4, 5, 1023, 1024, 1025, 4096, 4099, 20000, 100003])
 @pytest.mark.parametrize("kind", ["sparse", "dense", "wide", "zeros", "runs", "extreme"])
 def test_rlgamma_encode_bytes_match_oracle(gpu, P, kind):
   rng = np.random.default_rng(P * 31 + len(kind))

@@ -42,9 +42,9 @@ tiles = C * codec.num_tiles(P)
 if not HAVE:
   print("encode %.2f ms (no stamps in this build)" % (dt * 1e3))
   sys.exit(0)
-names = ["ticket+barrier", "A load+quantize", "B maxscan+barrier", "C lengths+barrier",
-         "D tail+barrier", "E lookback+barrier", "F emit+store"]
-tot = sum(buf[i] for i in range(7))
+names = ["loop/ticket+load", "A quant+code", "B-D scans+emit", "D tail+reductions",
+         "E lookback+publish", "F store"]
+tot = sum(buf[i] for i in range(len(names)))
 print("encode %.2f ms, %d tiles, %.0f cycles/tile total (memtime units)" % (dt * 1e3, tiles, tot / tiles))
 for i, n in enumerate(names):
   print("  %-22s %8.0f  %5.1f%%" % (n, buf[i] / tiles, 100.0 * buf[i] / tot))
