@@ -352,14 +352,21 @@ __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgc
 
 // Decoupled look-back for tile t of one client, run by one full wave.  Returns
 // the exclusive prefix (a root segment: body = stream bits before tile t).
+// pre1/pre2 (optional): this lane's status of tile t-1-lane, loaded earlier.
 __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int lane,
-                                        uint32_t* spin_err, bool& slow) {
+                                        uint32_t* spin_err, bool& slow, bool have_pre = false,
+                                        uint64_t pre1 = 0, uint64_t pre2 = 0) {
   Seg S = seg_identity();
   int64_t base = (int64_t)t - 1;
   for (;;) {
     const int64_t ti = base - lane;
     uint64_t w1 = kFlagPre, w2 = kFlagPre;  // ti < 0: virtual root prefix
     bool valid = ti < 0;
+    if (have_pre && base == (int64_t)t - 1 && !valid) {
+      w1 = pre1;
+      w2 = pre2;
+      valid = (w1 >> 62) != 0 && (w1 >> 62) == (w2 >> 62);
+    }
     int k;
     uint32_t spins = 0;
     for (;;) {
@@ -858,241 +865,290 @@ __device__ __forceinline__ void slow_emit(const EncodeArgs& a, const ClientQ& cq
 
 // One wavefront = one workgroup = one 1024-element tile at a time: no barriers,
 // every cross-lane step is DPP / ballot / readlane, the bit window is the
-// wave's own LDS; independent waves hide each other's latencies.
+// wave's own LDS.  Software-pipelined over the wave's tiles: tile n is
+// quantised, coded and its aggregate published, then tile n-1 (whose
+// predecessor status was fetched before tile n's work) finishes its look-back
+// and stores its words -- so the look-back's memory round trip overlaps a
+// whole tile of compute instead of stalling the wave.
 template <int MODE, bool INT_IN, bool RCP>
 __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs a) {
-  __shared__ uint32_t win[kWinWords + 3];  // + guard words for out-of-window emission
-  __shared__ uint32_t tailw;
+  __shared__ uint32_t wins[2][kWinWords + 3];  // double-buffered; + guard words
   const int lane = threadIdx.x;
   const uint32_t total_tiles = (uint32_t)a.nclients * (uint32_t)a.T;
   const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
   const bool pre = !INT_IN && a.prescale != nullptr;
+  const int64_t P = a.P;
 #ifdef FC_STAMPS
   uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
-  for (int i = lane; i < kWinWords + 3; i += kEncThreads) win[i] = 0;
+  for (int i = lane; i < 2 * (kWinWords + 3); i += kEncThreads) (&wins[0][0])[i] = 0;
   const uint32_t shard = blockIdx.x % a.nshards;
   uint32_t* my_counter = a.counter + kShardStride * shard;
   uint32_t tk = 0;
   if (lane == 0) tk = atomicAdd(my_counter, 1u);
   uint32_t ticket = shard + a.nshards * uniform(tk);
+  // the pending tile (coded, aggregate published, words not yet stored)
+  bool pv = false;
+  int32_t pt = 0, pc = 0, pfirst = 0, plast = -1;
+  uint32_t pbody = 0, ptail = 0;
+  uint32_t buf = 0;
 
-  while (ticket < total_tiles) {
+  for (;;) {
+    const bool have = ticket < total_tiles;
+    if (!have && !pv) break;
     STAMP(0);
-    // tickets interleave clients (tile-major) so each client has few tiles in flight
-    const int32_t t = (int32_t)(ticket / (uint32_t)a.nclients);
-    const int32_t c = (int32_t)(ticket - (uint32_t)t * (uint32_t)a.nclients);
-    const int64_t P = a.P;
-    const int64_t tile_base = (int64_t)t * kTE;
-    const bool last_tile = (t == a.T - 1);
-    const bool full = tile_base + kTE <= P;
-    const ClientParam cp = ld_param(cparams + c);
-    // raw values: chunk j of this lane = tile elements [256 j + 4 lane, +4)
-    uint32_t raw[kChunks][4];
-#pragma unroll
-    for (int j = 0; j < kChunks; ++j) {
-      const int64_t e0 = tile_base + 256 * j + 4 * lane;
-      if (full) {
-        const uint4 v = *(const uint4*)(cp.x + e0);
-        raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) raw[j][k] = (e0 + k < P) ? cp.x[e0 + k] : 0u;
-      }
-    }
     uint32_t ntk = 0;
-    if (lane == 0) ntk = atomicAdd(my_counter, 1u);  // next ticket, used after phase D
-    // predecessor's status, fetched now so that the common case (its inclusive
-    // prefix is already published) costs no round trip at the look-back
-    uint64_t pw1 = 0, pw2 = 0;
-    if (t > 0) {
-      const uint64_t* sp = a.status + 2 * ((int64_t)c * a.T + t - 1);
+    if (have && lane == 0) ntk = atomicAdd(my_counter, 1u);  // next ticket
+    // the pending tile's look-back window (lane i: tile pt-1-i), fetched now and
+    // used after this tile's work
+    uint64_t pw1 = kFlagPre, pw2 = kFlagPre;
+    if (pv && pt > lane) {
+      const uint64_t* sp = a.status + 2 * ((int64_t)pc * a.T + pt - 1 - lane);
       pw1 = ld_agent(sp);
       pw2 = ld_agent(sp + 1);
     }
-
-    // ---- A: quantise + chunk-local codes ----
-    ChunkCode cc[kChunks];
-    float dist = 0.0f;
-    int32_t nnz = 0;
-    {
-      const ClientQ cq = client_q_of(cp, pre);
+    // ---- this tile: A-D, then publish its aggregate ----
+    bool nv = false;
+    int32_t nt_ = 0, nc = 0, nfirst = 0, nlast = -1;
+    uint32_t nbody = 0, ntail = 0;
+    uint32_t next = ticket;
+    if (have) {
+      uint32_t* win = wins[buf];
+      // tickets interleave clients (tile-major) so each client has few tiles in flight
+      const int32_t t = (int32_t)(ticket / (uint32_t)a.nclients);
+      const int32_t c = (int32_t)(ticket - (uint32_t)t * (uint32_t)a.nclients);
+      const int64_t tile_base = (int64_t)t * kTE;
+      const bool full = tile_base + kTE <= P;
+      const ClientParam cp = ld_param(cparams + c);
+      // raw values: chunk j of this lane = tile elements [256 j + 4 lane, +4)
+      uint32_t raw[kChunks][4];
 #pragma unroll
       for (int j = 0; j < kChunks; ++j) {
-        const int32_t rel0 = 256 * j + 4 * lane;
-        if (INT_IN || (FC_ABL & 8)) {
-          int32_t q4[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) q4[k] = (FC_ABL & 8) ? (int32_t)(raw[j][k] >> 29) - 3 : (int32_t)raw[j][k];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
-          cc[j] = chunk_local(q4, rel0);
+        const int64_t e0 = tile_base + 256 * j + 4 * lane;
+        if (full) {
+          const uint4 v = *(const uint4*)(cp.x + e0);
+          raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
         } else {
-          const uint32_t g = (uint32_t)((tile_base + rel0) >> 2);
-          if (MODE == FC_DITHERED && !full)
-            cc[j] = quant_code_fast<MODE, RCP, true>(cq, g, raw[j], rel0, dist, nnz,
-                                                     (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - rel0)));
-          else
-            cc[j] = quant_code_fast<MODE, RCP>(cq, g, raw[j], rel0, dist, nnz);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) raw[j][k] = (e0 + k < P) ? cp.x[e0 + k] : 0u;
         }
-        __builtin_amdgcn_sched_barrier(0);  // one chunk at a time: bounded mask/VGPR pressure
       }
-    }
-    STAMP(1);
-
-    // ---- B: last nonzero before each chunk (4 interleaved max-scans over
-    //      (chunk, lane) order), then the chunks' run-code prepends ----
-    int32_t carry = -1, wfirst = 0x7FFFFFFF;
-    uint32_t lng = 0;
-    {
-      int32_t im[kChunks];
-#pragma unroll
-      for (int j = 0; j < kChunks; ++j) im[j] = cc[j].last;
-      dpp_incl_max4(im);
-#pragma unroll
-      for (int j = 0; j < kChunks; ++j) {
-        const int32_t prev = max(dpp_shr1(im[j], -1), carry);
-        carry = max(carry, lane63(im[j]));
-        wfirst = min(wfirst, cc[j].first >= 0 ? cc[j].first : 0x7FFFFFFF);
-        chunk_prepend(cc[j], prev);
-        lng |= cc[j].lng;
+      // ---- A: quantise + chunk-local codes ----
+      ChunkCode cc[kChunks];
+      float dist = 0.0f;
+      int32_t nnz = 0;
+      {
+        const ClientQ cq = client_q_of(cp, pre);
+  #pragma unroll
+        for (int j = 0; j < kChunks; ++j) {
+          const int32_t rel0 = 256 * j + 4 * lane;
+          if (INT_IN || (FC_ABL & 8)) {
+            int32_t q4[4];
+  #pragma unroll
+            for (int k = 0; k < 4; ++k) q4[k] = (FC_ABL & 8) ? (int32_t)(raw[j][k] >> 29) - 3 : (int32_t)raw[j][k];
+  #pragma unroll
+            for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
+            cc[j] = chunk_local(q4, rel0);
+          } else {
+            const uint32_t g = (uint32_t)((tile_base + rel0) >> 2);
+            if (MODE == FC_DITHERED && !full)
+              cc[j] = quant_code_fast<MODE, RCP, true>(cq, g, raw[j], rel0, dist, nnz,
+                                                       (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - rel0)));
+            else
+              cc[j] = quant_code_fast<MODE, RCP>(cq, g, raw[j], rel0, dist, nnz);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one chunk at a time: bounded mask/VGPR pressure
+        }
       }
-    }
-    // ---- C: body-relative offsets (two packed 16-bit sum-scans) ----
-    uint32_t off[kChunks];
-    uint32_t body;
-    {
-      uint32_t s2[2] = {cc[0].len | (cc[1].len << 16), cc[2].len | (cc[3].len << 16)};
-      dpp_incl_sum2(s2);
-      const uint32_t t0 = (uint32_t)lane63((int32_t)s2[0]), t1 = (uint32_t)lane63((int32_t)s2[1]);
-      const uint32_t b1 = t0 & 0xFFFFu, b2 = b1 + (t0 >> 16), b3 = b2 + (t1 & 0xFFFFu);
-      off[0] = (s2[0] & 0xFFFFu) - cc[0].len;
-      off[1] = b1 + (s2[0] >> 16) - cc[1].len;
-      off[2] = b2 + (s2[1] & 0xFFFFu) - cc[2].len;
-      off[3] = b3 + (s2[1] >> 16) - cc[3].len;
-      body = b3 + (t1 >> 16);
-    }
-    // fast path: whole tile inside the tensor (or int input), no long chunk, and
-    // prefix + body + trailing code + one funnel word fit the wave's window
-    const bool fast = __ballot(lng != 0) == 0 && kPre + body + 96u <= 32u * kWinWords;
-    // ---- D: emit (body-relative) ----
-    if (FC_ABL & 1) {
-      asm volatile("" :: "v"((uint32_t)cc[0].acc), "v"((uint32_t)cc[3].acc), "v"(off[0]), "v"(off[3]));
-    } else {
-#pragma unroll
-      for (int j = 0; j < kChunks; ++j) emit64(win, cc[j].acc, cc[j].len, kPre + off[j]);
-    }
-    STAMP(2);
+      STAMP(1);
 
-    const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;  // body's last 32 bits
-    const int32_t tile_last = carry;
-    const int32_t tile_first = wave_min_i(wfirst);
-    if (fast) {
-      const float d = wave_sum_f(dist);
-      const int32_t n = wave_sum_i(nnz);
-      if (lane == 0) {
-        if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
-        if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t] = n;
+      // ---- B: last nonzero before each chunk (4 interleaved max-scans over
+      //      (chunk, lane) order), then the chunks' run-code prepends ----
+      int32_t carry = -1, wfirst = 0x7FFFFFFF;
+      uint32_t lng = 0;
+      {
+        int32_t im[kChunks];
+  #pragma unroll
+        for (int j = 0; j < kChunks; ++j) im[j] = cc[j].last;
+        dpp_incl_max4(im);
+  #pragma unroll
+        for (int j = 0; j < kChunks; ++j) {
+          const int32_t prev = max(dpp_shr1(im[j], -1), carry);
+          carry = max(carry, lane63(im[j]));
+          wfirst = min(wfirst, cc[j].first >= 0 ? cc[j].first : 0x7FFFFFFF);
+          chunk_prepend(cc[j], prev);
+          lng |= cc[j].lng;
+        }
       }
-    }
-    const uint32_t next = shard + a.nshards * uniform(ntk);
-    STAMP(3);
+      // ---- C: body-relative offsets (two packed 16-bit sum-scans) ----
+      uint32_t off[kChunks];
+      uint32_t body;
+      {
+        uint32_t s2[2] = {cc[0].len | (cc[1].len << 16), cc[2].len | (cc[3].len << 16)};
+        dpp_incl_sum2(s2);
+        const uint32_t t0 = (uint32_t)lane63((int32_t)s2[0]), t1 = (uint32_t)lane63((int32_t)s2[1]);
+        const uint32_t b1 = t0 & 0xFFFFu, b2 = b1 + (t0 >> 16), b3 = b2 + (t1 & 0xFFFFu);
+        off[0] = (s2[0] & 0xFFFFu) - cc[0].len;
+        off[1] = b1 + (s2[0] >> 16) - cc[1].len;
+        off[2] = b2 + (s2[1] & 0xFFFFu) - cc[2].len;
+        off[3] = b3 + (s2[1] >> 16) - cc[3].len;
+        body = b3 + (t1 >> 16);
+      }
+      // fast path: whole tile inside the tensor (or int input), no long chunk, and
+      // prefix + body + trailing code + one funnel word fit the wave's window
+      const bool fast = __ballot(lng != 0) == 0 && kPre + body + 96u <= 32u * kWinWords;
+      // ---- D: emit (body-relative) ----
+      if (FC_ABL & 1) {
+        asm volatile("" :: "v"((uint32_t)cc[0].acc), "v"((uint32_t)cc[3].acc), "v"(off[0]), "v"(off[3]));
+      } else {
+  #pragma unroll
+        for (int j = 0; j < kChunks; ++j) emit64(win, cc[j].acc, cc[j].len, kPre + off[j]);
+      }
+      STAMP(2);
 
-    // ---- E: decoupled look-back ----
-    uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t);
-    Seg agg;
-    agg.has_nz = tile_last >= 0;
-    agg.first = agg.has_nz ? (int32_t)(tile_base + tile_first) : 0;
-    agg.last = agg.has_nz ? (int32_t)(tile_base + tile_last) : 0;
-    agg.body = body;
-    agg.tail = agg_tail;
-    bool slow = !fast;
-    Seg excl = seg_identity();
-    if (!slow) {
-      if (t == 0) {
-        excl.has_nz = 1;
-        excl.first = -1;
-        excl.last = -1;
-      } else if ((pw1 >> 62) == 2 && (pw2 >> 62) == 2) {
-        excl = seg_from_status(pw1, pw2, 0);  // predecessor's inclusive prefix
-      } else if ((pw1 >> 62) == 3 && (pw2 >> 62) == 3) {
-        slow = true;  // predecessor left to the exact kernel
+      const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;
+      const int32_t tile_last = carry;
+      const int32_t tile_first = wave_min_i(wfirst);
+      if (fast) {
+        const float d = wave_sum_f(dist);
+        const int32_t n = wave_sum_i(nnz);
+        if (lane == 0) {
+          if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
+          if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t] = n;
+        }
+      }
+      next = shard + a.nshards * uniform(ntk);
+      STAMP(3);
+      uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t);
+      if (!fast) {
+        // a code past the fast path's limits or a body beyond the window: the
+        // client is re-encoded by k_encode_exact
+        if (lane == 0) {
+          st_agent(st + 1, kFlagSlow);
+          st_agent(st, kFlagSlow);
+          if (atomicOr(&a.slow_flag[c], 1) == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = c;
+        }
+        for (int i = lane; i < kWinWords; i += kEncThreads) win[i] = 0;
       } else {
         if (lane == 0) {
-          const uint64_t fr = agg.has_nz ? (uint64_t)tile_first : kNoPos;
-          const uint64_t lr = agg.has_nz ? (uint64_t)tile_last : kNoPos;
-          st_agent(st + 1, kFlagAgg | agg.tail);
-          st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
+          if (t == 0) {  // chain root: the inclusive prefix right away
+            Seg root = seg_identity(), agg;
+            root.has_nz = 1;
+            root.first = root.last = -1;
+            agg.has_nz = tile_last >= 0;
+            agg.first = agg.has_nz ? tile_first : 0;
+            agg.last = agg.has_nz ? tile_last : 0;
+            agg.body = body;
+            agg.tail = agg_tail;
+            const Seg incl = seg_combine(root, agg);
+            st_agent(st + 1, kFlagPre | incl.tail);
+            st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+          } else {
+            const uint64_t fr = tile_last >= 0 ? (uint64_t)tile_first : kNoPos;
+            const uint64_t lr = tile_last >= 0 ? (uint64_t)tile_last : kNoPos;
+            st_agent(st + 1, kFlagAgg | agg_tail);
+            st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
+          }
         }
-        if (FC_ABL & 4) {
-          excl.has_nz = 1;
-          excl.first = excl.last = -1;
-        } else {
-          excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, a.spin_err, slow);
-        }
+        nv = true;
+        nt_ = t;
+        nc = c;
+        nfirst = tile_first;
+        nlast = tile_last;
+        nbody = body;
+        ntail = agg_tail;
       }
-    }
-    if (slow) {
-      // this tile (a long code or a body beyond the window), or one before it, is
-      // re-encoded by k_encode_exact together with the rest of the client
-      if (lane == 0) {
-        st_agent(st + 1, kFlagSlow);
-        st_agent(st, kFlagSlow);
-        if (atomicOr(&a.slow_flag[c], 1) == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = c;
-      }
-      for (int i = lane; i < kWinWords; i += kEncThreads) win[i] = 0;
-      ticket = next;
-      continue;
-    }
-    const Seg incl = seg_combine(excl, agg);
-    const uint32_t r0 = (uint32_t)(excl.body & 31);
-    const uint32_t dfirst = agg.has_nz ? (uint32_t)(agg.first - excl.last) : 0u;
-    const uint32_t R0 = agg.has_nz ? glen(dfirst) : 0u;
-    const uint32_t bstart = r0 + R0;  // stream-window bit where the body starts
-    const uint32_t tb = excl.tail & (r0 ? ((1u << r0) - 1u) : 0u);
-    uint32_t trail_len = 0;
-    uint64_t trail = 0;
-    if (last_tile) {
-      const int64_t zc = P - 1 - (int64_t)incl.last;  // trailing zeros
-      if (zc > 0) {
-        trail = (uint64_t)(zc + 1);
-        trail_len = 2u * (63u - (uint32_t)__clzll(trail)) + 1u;
-      }
-    }
-    if (lane == 0) {
-      st_agent(st + 1, kFlagPre | incl.tail);
-      st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
-      const int64_t ib = (int64_t)c * (a.T + 1);
-      a.idx[ib + t] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
-      if (last_tile) {
-        a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
-        a.total_bits[c] = (int64_t)incl.body + trail_len;
-      }
-      // leading pieces just before the body, trailing code after it
-      emit64(win, tb, r0, kPre - bstart);
-      emit64(win, dfirst, R0, kPre - R0);
-      if (trail_len) emit64(win, trail, trail_len, kPre + body);
     }
     STAMP(4);
 
-    // ---- F: store the words this tile owns ----
-    const uint32_t nwin_bits = bstart + body + trail_len;
-    const uint32_t nwords_owned = last_tile ? (nwin_bits + 31) / 32 : nwin_bits / 32;
-    const int64_t cap = cp.cap;
-    uint32_t* out32 = cp.out;
-    const uint64_t w0 = excl.body >> 5;
-    if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&a.overflow[c], 1u);
-    const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
-    for (uint32_t k = lane; k < nwords_owned; k += kEncThreads) {
-      const uint32_t wv32 = win_bits32(win, s0 + 32 * k);
-      if (FC_ABL & 2) asm volatile("" :: "v"(wv32));
-      else if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
+    // ---- the pending tile: look-back, publish its prefix, store its words ----
+    if (pv) {
+      uint32_t* win = wins[buf ^ 1];
+      const int64_t tile_base = (int64_t)pt * kTE;
+      const bool last_tile = (pt == a.T - 1);
+      uint64_t* st = a.status + 2 * ((int64_t)pc * a.T + pt);
+      Seg agg;
+      agg.has_nz = plast >= 0;
+      agg.first = agg.has_nz ? (int32_t)(tile_base + pfirst) : 0;
+      agg.last = agg.has_nz ? (int32_t)(tile_base + plast) : 0;
+      agg.body = pbody;
+      agg.tail = ptail;
+      bool slow = false;
+      Seg excl = seg_identity();
+      if (pt == 0 || (FC_ABL & 4)) {
+        excl.has_nz = 1;
+        excl.first = excl.last = -1;
+      } else {
+        excl = lookback(a.status + 2 * (int64_t)pc * a.T, pt, lane, a.spin_err, slow, true, pw1, pw2);
+      }
+      if (slow) {
+        if (lane == 0) {
+          st_agent(st + 1, kFlagSlow);
+          st_agent(st, kFlagSlow);
+          if (atomicOr(&a.slow_flag[pc], 1) == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = pc;
+        }
+        for (int i = lane; i < kWinWords; i += kEncThreads) win[i] = 0;
+      } else {
+        const Seg incl = seg_combine(excl, agg);
+        const uint32_t r0 = (uint32_t)(excl.body & 31);
+        const uint32_t dfirst = agg.has_nz ? (uint32_t)(agg.first - excl.last) : 0u;
+        const uint32_t R0 = agg.has_nz ? glen(dfirst) : 0u;
+        const uint32_t bstart = r0 + R0;  // stream-window bit where the body starts
+        const uint32_t tb = excl.tail & (r0 ? ((1u << r0) - 1u) : 0u);
+        uint32_t trail_len = 0;
+        uint64_t trail = 0;
+        if (last_tile) {
+          const int64_t zc = P - 1 - (int64_t)incl.last;  // trailing zeros
+          if (zc > 0) {
+            trail = (uint64_t)(zc + 1);
+            trail_len = 2u * (63u - (uint32_t)__clzll(trail)) + 1u;
+          }
+        }
+        if (lane == 0) {
+          if (pt > 0) {
+            st_agent(st + 1, kFlagPre | incl.tail);
+            st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+          }
+          const int64_t ib = (int64_t)pc * (a.T + 1);
+          a.idx[ib + pt] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
+          if (last_tile) {
+            a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
+            a.total_bits[pc] = (int64_t)incl.body + trail_len;
+          }
+          // leading pieces just before the body, trailing code after it
+          emit64(win, tb, r0, kPre - bstart);
+          emit64(win, dfirst, R0, kPre - R0);
+          if (trail_len) emit64(win, trail, trail_len, kPre + pbody);
+        }
+        STAMP(5);
+        const ClientParam cp = ld_param(cparams + pc);
+        const uint32_t nwin_bits = bstart + pbody + trail_len;
+        const uint32_t nwords_owned = last_tile ? (nwin_bits + 31) / 32 : nwin_bits / 32;
+        const int64_t cap = cp.cap;
+        uint32_t* out32 = cp.out;
+        const uint64_t w0 = excl.body >> 5;
+        if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&a.overflow[pc], 1u);
+        const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
+        for (uint32_t k = lane; k < nwords_owned; k += kEncThreads) {
+          const uint32_t wv32 = win_bits32(win, s0 + 32 * k);
+          if (FC_ABL & 2) asm volatile("" :: "v"(wv32));
+          else if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
+        }
+        const uint32_t nt = min((uint32_t)kWinWords, (kPre + pbody + trail_len + 31) / 32 + 1);
+        for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
+      }
     }
-    const uint32_t nt = min((uint32_t)kWinWords, (kPre + body + trail_len + 31) / 32 + 1);
-    for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
-    STAMP(5);
-    ticket = next;
+    STAMP(6);
+    pv = nv;
+    pt = nt_;
+    pc = nc;
+    pfirst = nfirst;
+    plast = nlast;
+    pbody = nbody;
+    ptail = ntail;
+    buf ^= 1;
+    ticket = have ? next : ticket;
   }
 #ifdef FC_STAMPS
   if (lane == 0)

@@ -42,8 +42,8 @@ tiles = C * codec.num_tiles(P)
 if not HAVE:
   print("encode %.2f ms (no stamps in this build)" % (dt * 1e3))
   sys.exit(0)
-names = ["loop/ticket+load", "A quant+code", "B-D scans+emit", "D tail+reductions",
-         "E lookback+publish", "F store"]
+names = ["loop/ticket", "A load+quant+code", "B-D scans+emit", "D tail+reductions", "publish agg",
+         "pending lookback+prefix", "pending store"]
 tot = sum(buf[i] for i in range(len(names)))
 print("encode %.2f ms, %d tiles, %.0f cycles/tile total (memtime units)" % (dt * 1e3, tiles, tot / tiles))
 for i, n in enumerate(names):
