@@ -1402,6 +1402,142 @@ __device__ __forceinline__ uint32_t decode_code(BitReader& br, uint32_t& d, int3
   return 2u * (31u - __clz(d)) + 1u + 1u + 2u * (31u - __clz(m)) + 1u;
 }
 
+// General decode of one code at absolute bit position pos straight from
+// memory (any length; the rare path, kept out of line).  slow_code returns the
+// bits consumed, 0 on a malformed code.
+__device__ __forceinline__ uint32_t peek32(const uint32_t* w, uint64_t nw, uint64_t pos) {
+  const uint64_t i = pos >> 5;
+  const uint32_t o = (uint32_t)(pos & 31);
+  const uint32_t hi = i < nw ? bswap32(w[i]) : 0u;
+  const uint32_t lo = i + 1 < nw ? bswap32(w[i + 1]) : 0u;
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (32 - o));
+}
+// Elias-gamma value at bit q (advances q); 0 if malformed (> 31 leading zeros).
+__device__ __forceinline__ uint32_t gamma_at(const uint32_t* w, uint64_t nw, uint64_t& q) {
+  uint32_t zeros = 0;
+  for (;;) {
+    const uint32_t t = peek32(w, nw, q);
+    if (t) {
+      const uint32_t z = (uint32_t)__clz(t);
+      zeros += z;
+      q += z;
+      break;
+    }
+    zeros += 32;
+    q += 32;
+    if (zeros > 31 || (q >> 5) >= nw) return 0;
+  }
+  if (zeros > 31) return 0;
+  const uint32_t v = peek32(w, nw, q) >> (31 - zeros);  // zeros + 1 bits
+  q += zeros + 1;
+  return v;
+}
+struct CodeVal {
+  uint32_t L, d;
+  int32_t v;
+};
+__device__ __noinline__ CodeVal slow_code(const uint8_t* base, int64_t cap, uint64_t pos) {
+  const uint32_t* w = (const uint32_t*)base;
+  const uint64_t nw = (uint64_t)(cap >> 2);
+  uint64_t q = pos;
+  CodeVal r{0, 0, 0};
+  const uint32_t d = gamma_at(w, nw, q);
+  const uint32_t sg = peek32(w, nw, q) >> 31;
+  q += 1;
+  const uint32_t m = gamma_at(w, nw, q);
+  if (d == 0 || m == 0) return r;
+  r.L = (uint32_t)(q - pos);
+  r.d = d;
+  r.v = sg ? (int32_t)m : -(int32_t)m;
+  return r;
+}
+
+// One segment = one client's code for one 1024-element tile: bits [b0, b1),
+// previous nonzero at tile-relative position rel.  Bit reader: a 64-bit window
+// (MSB-aligned, > 32 valid bits), a 128-bit reservoir behind it and the next
+// 16-byte block already in flight.  Codes that fit the top 32 window bits are
+// decoded branch-free; longer ones go through slow_code and the reader
+// restarts after them.
+struct SegReader {
+  const uint4* p;
+  const uint4* end;
+  uint4 nx;
+  uint64_t win, rh, rl;
+  int32_t nwin, rb;
+  __device__ __forceinline__ void fetch() {
+    nx = *(p < end ? p : end - 1);  // clamped, unconditional: no branch before the wait
+    ++p;
+  }
+  __device__ __forceinline__ void take_block() {
+    rh = ((uint64_t)bswap32(nx.x) << 32) | bswap32(nx.y);
+    rl = ((uint64_t)bswap32(nx.z) << 32) | bswap32(nx.w);
+    rb = 128;
+    fetch();
+  }
+  __device__ __forceinline__ uint32_t pop32() {
+    const uint32_t w = (uint32_t)(rh >> 32);
+    rh = (rh << 32) | (rl >> 32);
+    rl <<= 32;
+    rb -= 32;
+    if (rb == 0) take_block();
+    return w;
+  }
+  __device__ __forceinline__ void init(const uint8_t* base, int64_t cap, uint64_t bit) {
+    p = (const uint4*)base + (bit >> 7);
+    end = (const uint4*)base + (cap >> 4);
+    fetch();
+    take_block();
+    for (int i = (int)((bit >> 5) & 3); i > 0; --i) (void)pop32();
+    win = (uint64_t)pop32() << 32;
+    win |= pop32();
+    const int skip = (int)(bit & 31);
+    win <<= skip;
+    nwin = 64 - skip;
+  }
+};
+
+__device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
+                                               uint64_t b1, int32_t rel, int32_t* my, int32_t* err) {
+  SegReader r;
+  r.init(base, cap, b0);
+  uint64_t pos = b0;
+  uint32_t bad = 0;
+  while (pos < b1) {
+    const uint32_t top = (uint32_t)(r.win >> 32);
+    const uint32_t z1 = (uint32_t)__clz(top);
+    const uint32_t sa = 30u - 2u * z1;        // sign-bit position
+    const uint32_t rest = top << (32u - sa);  // bits after the sign bit
+    const uint32_t z2 = (uint32_t)__clz(rest);
+    uint32_t L = 2u * (z1 + z2) + 3u;
+    uint32_t d = top >> (sa + 1u);
+    const uint32_t m = rest >> (31u - 2u * z2);
+    int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
+    if (L <= 32u) {
+      r.win <<= L;
+      r.nwin -= (int32_t)L;
+      if (r.nwin <= 32) {
+        r.win |= (uint64_t)r.pop32() << (32 - r.nwin);
+        r.nwin += 32;
+      }
+    } else {  // rare: a code longer than 32 bits (or a malformed one)
+      const CodeVal cv = slow_code(base, cap, pos);
+      if (cv.L == 0) {
+        bad = 1;
+        break;
+      }
+      L = cv.L;
+      d = cv.d;
+      v = cv.v;
+      r.init(base, cap, pos + L);
+    }
+    pos += L;
+    rel += (int32_t)d;
+    bad |= (uint32_t)rel >= (uint32_t)kTE;
+    atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v);
+  }
+  if (bad || pos != b1) atomicOr(err, 1);
+}
+
 __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
   extern __shared__ int32_t acc[];  // [tiles_per_wg][kTE]
   const int tid = threadIdx.x;
@@ -1420,22 +1556,8 @@ __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
       const uint64_t e0 = a.idx[ib], e1 = a.idx[ib + 1];
       const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
       if (bend <= bstart) continue;
-      int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
-      BitReader br;
-      br.init(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart);
-      int64_t rem = (int64_t)(bend - bstart);
-      while (rem > 0) {
-        uint32_t d;
-        int32_t v;
-        const uint32_t L = decode_code(br, d, v);
-        rel += (int32_t)d;
-        if (L == 0 || (uint32_t)rel >= (uint32_t)kTE) {
-          atomicOr(a.err, 1);
-          break;
-        }
-        atomicAdd(&my[rel], v);
-        rem -= L;
-      }
+      const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
+      decode_segment(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart, bend, rel, my, a.err);
     }
   }
   __syncthreads();
