@@ -31,6 +31,9 @@
 #ifndef FC_ENC_WAVES
 #define FC_ENC_WAVES 5  // encoder waves per SIMD the register budget is sized for
 #endif
+#ifndef FC_CHUNK_BARRIER
+#define FC_CHUNK_BARRIER __builtin_amdgcn_sched_barrier(0)
+#endif
 #ifndef FC_ABL
 #define FC_ABL 0
 #endif
@@ -250,7 +253,14 @@ struct EncodeArgs {
   int32_t* slow_flag;    // [nclients] (zeroed per launch)
   int32_t* slow_list;    // [nclients]
   uint32_t* counter2;    // exact kernel's ticket counter
+  uint32_t div_m, div_l;  // ticket / nclients by multiply-high (Granlund-Montgomery)
 };
+
+__device__ __forceinline__ uint32_t div_clients(const EncodeArgs& a, uint32_t n) {
+  if (a.div_l == 0) return n;  // nclients == 1
+  const uint32_t t1 = __umulhi(n, a.div_m);
+  return (t1 + ((n - t1) >> 1)) >> (a.div_l - 1);
+}
 
 // Emit a piece of <= 32 bits at window bit position wp into the LDS window
 // covering window words [pass_lo, pass_lo + kWinWords).
@@ -412,6 +422,101 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
   return S;
 }
 
+#ifdef FC_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define FC_COUNT(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_stamps[i], (unsigned long long)(v)); } while (0)
+#else
+#define FC_COUNT(i, v) do {} while (0)
+#endif
+// Vectorised look-back (the encoder's common case).  Lane i holds tile
+// t-64+i (lane 63 = t-1); pre1/pre2 are those statuses, loaded earlier.  Once
+// the nearest inclusive prefix p and every aggregate after it are visible, the
+// fold is two DPP scans instead of a serial scalar walk: the last nonzero
+// before each aggregate (max-scan of the aggregates' last positions), its
+// first run code length, and the sum of bodies.  The combined tail is the
+// newest tile's tail whenever that tile's body has >= 32 bits; otherwise (and
+// when no prefix is within 64 tiles) the scalar lookback() does the fold.
+__device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t, int lane,
+                                            uint32_t* spin_err, bool& slow, uint64_t pre1,
+                                            uint64_t pre2) {
+  const int64_t ti = (int64_t)t - 64 + lane;
+  uint64_t w1 = kFlagPre, w2 = kFlagPre;  // ti < 0: virtual root prefix (last = -1, body 0)
+  bool valid = ti < 0;
+  if (!valid) {
+    w1 = pre1;
+    w2 = pre2;
+    valid = (w1 >> 62) != 0 && (w1 >> 62) == (w2 >> 62);
+  }
+  uint32_t spins = 0;
+  int p;
+  for (;;) {
+    const uint64_t pre = __ballot(valid && (w1 >> 62) >= 2);
+    const uint64_t val = __ballot(valid);
+    if (pre == 0) {  // no prefix within 64 tiles: scalar walk
+      FC_COUNT(10, 1);
+      return lookback(status_c, t, lane, spin_err, slow);
+    }
+    p = 63 - (int)__clzll(pre);  // nearest (newest) prefix
+    const uint64_t need = ~0ull << p;
+    if ((val & need) == need) break;
+    FC_COUNT(9, 1);
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 24)) {
+      if (lane == 0) atomicOr(spin_err, 1u);
+      Seg r = seg_identity();
+      r.has_nz = 1;
+      r.first = r.last = -1;
+      return r;
+    }
+    if (!valid) {
+      w1 = ld_agent(status_c + 2 * ti);
+      w2 = ld_agent(status_c + 2 * ti + 1);
+      valid = (w1 >> 62) != 0 && (w1 >> 62) == (w2 >> 62);
+    }
+  }
+  const uint32_t w1hi = (uint32_t)(w1 >> 32);
+  if ((__builtin_amdgcn_readlane(w1hi, p) >> 30) == 3u) {  // a slow tile: give up
+    slow = true;
+    return seg_identity();
+  }
+  Seg r;
+  r.has_nz = 1;
+  r.first = -1;
+  FC_COUNT(8, 1);
+  FC_COUNT(13, 63 - p);
+  if (p == 63) {  // the predecessor's own inclusive prefix
+    FC_COUNT(12, 1);
+    r.last = (int32_t)((__builtin_amdgcn_readlane(w1hi, 63) >> 4) & ((1u << 26) - 1)) - 1;
+    r.body = ((uint64_t)(__builtin_amdgcn_readlane(w1hi, 63) & 0xFu) << 32) |
+             __builtin_amdgcn_readlane((uint32_t)w1, 63);
+    r.tail = __builtin_amdgcn_readlane((uint32_t)w2, 63);
+    return r;
+  }
+  // per-lane decode: prefix lane p, aggregates above it, nothing below
+  const bool agg = lane > p;
+  const uint32_t fr = (uint32_t)(w1 >> 49) & 0x1FFF, lr = (uint32_t)(w1 >> 36) & 0x1FFF;
+  const bool nz = agg && fr != kNoPos;
+  const int32_t tb = (int32_t)(ti * kTE);
+  int32_t lastv = -1;
+  if (lane == p) lastv = (int32_t)((w1 >> 36) & ((1u << 26) - 1)) - 1;
+  if (nz) lastv = tb + (int32_t)lr;
+  const int32_t M = dpp_incl_max(lastv);
+  const int32_t Mx = dpp_shr1(M, -1);  // last nonzero before this tile
+  const uint32_t abody = (uint32_t)(w1 & kMask36);
+  uint32_t contrib = agg ? abody : 0u;
+  if (nz) contrib += glen((uint32_t)(tb + (int32_t)fr - Mx));
+  const uint32_t csum = (uint32_t)wave_sum_i((int32_t)contrib);
+  r.last = lane63(M);
+  r.body = (((uint64_t)(__builtin_amdgcn_readlane(w1hi, p) & 0xFu) << 32) |
+            __builtin_amdgcn_readlane((uint32_t)w1, p)) + csum;
+  if (__builtin_amdgcn_readlane(abody, 63) >= 32u) {
+    r.tail = __builtin_amdgcn_readlane((uint32_t)w2, 63);
+    return r;
+  }
+  FC_COUNT(11, 1);
+  return lookback(status_c, t, lane, spin_err, slow);  // short newest body: exact scalar fold
+}
+
 // Runtime-indexed read of a small register array without scratch (select chain).
 template <typename T, int N>
 __device__ __forceinline__ T pick(const T (&arr)[N], int j) {
@@ -501,7 +606,7 @@ __device__ __forceinline__ ChunkCode chunk_local(const int32_t (&q4)[4], int32_t
 // its exponent, and the in-chunk run lengths come from select chains on the
 // nonzero flags.  |r| >= 8192, Inf or NaN marks the chunk long; the slow path
 // then recomputes the tile exactly (TF cast semantics, codes of any length).
-template <int MODE, bool RCP, bool MASK = false>
+template <int MODE, bool RCP, bool PRE, bool MASK = false>
 __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t g,
                                                      const uint32_t (&r4)[4], int32_t rel0,
                                                      float& dist, int32_t& nnz, int32_t nvalid = 4) {
@@ -514,7 +619,7 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     float xv = __uint_as_float(r4[k]);
-    if (cq.pre) xv = (xv * cq.s0) * cq.s1;
+    if (PRE) xv = (xv * cq.s0) * cq.s1;
     const float sc = RCP ? xv * cq.rcp : xv / cq.step;
     float r, noise = 0.0f;
     if (MODE == FC_UNIFORM) {
@@ -551,8 +656,11 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
     const uint32_t m = (uint32_t)fabsf(q[k]);
     const uint32_t ml = 2u * ((__float_as_uint(q[k]) >> 23) & 0xFFu) - 253u;  // 2 floor(log2 m) + 1
     const uint32_t t = 2u * dv[k] + (q[k] > 0.0f ? 1u : 0u);                     // run code, sign bit
-    const uint32_t code = nz[k] ? ((t << ml) | m) : 0u;
-    const uint32_t L = nz[k] ? rl[k] + ml + 1u : 0u;
+    // zero elements emit nothing: masked, not branched (keeps the wave convergent)
+    uint32_t mk = nz[k] ? 0xFFFFFFFFu : 0u;
+    asm volatile("" : "+v"(mk));
+    const uint32_t code = ((t << ml) | m) & mk;
+    const uint32_t L = (rl[k] + ml + 1u) & mk;
     r.acc = k == 0 ? (uint64_t)code : ((r.acc << L) | code);
     r.len += L;
   }
@@ -593,7 +701,6 @@ __device__ __forceinline__ void put(T (&arr)[N], int j, T v) {
 }
 
 #ifdef FC_STAMPS
-__device__ unsigned long long g_stamps[8];
 #define STAMP(i)                                               \
   do {                                                         \
     if (lane == 0) {                                           \
@@ -870,13 +977,13 @@ __device__ __forceinline__ void slow_emit(const EncodeArgs& a, const ClientQ& cq
 // predecessor status was fetched before tile n's work) finishes its look-back
 // and stores its words -- so the look-back's memory round trip overlaps a
 // whole tile of compute instead of stalling the wave.
-template <int MODE, bool INT_IN, bool RCP>
+template <int MODE, bool INT_IN, bool RCP, bool PRE>
 __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs a) {
   __shared__ uint32_t wins[2][kWinWords + 3];  // double-buffered; + guard words
   const int lane = threadIdx.x;
   const uint32_t total_tiles = (uint32_t)a.nclients * (uint32_t)a.T;
   const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
-  const bool pre = !INT_IN && a.prescale != nullptr;
+  constexpr bool pre = PRE;
   const int64_t P = a.P;
 #ifdef FC_STAMPS
   uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -886,8 +993,10 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
   const uint32_t shard = blockIdx.x % a.nshards;
   uint32_t* my_counter = a.counter + kShardStride * shard;
   uint32_t tk = 0;
-  if (lane == 0) tk = atomicAdd(my_counter, 1u);
+  if (FC_ABL & 512) tk = blockIdx.x / a.nshards;
+  else if (lane == 0) tk = atomicAdd(my_counter, 1u);
   uint32_t ticket = shard + a.nshards * uniform(tk);
+  const uint32_t tk_step = (gridDim.x + a.nshards - 1 - shard) / a.nshards;  // blocks on this shard
   // the pending tile (coded, aggregate published, words not yet stored)
   bool pv = false;
   int32_t pt = 0, pc = 0, pfirst = 0, plast = -1;
@@ -899,12 +1008,13 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
     if (!have && !pv) break;
     STAMP(0);
     uint32_t ntk = 0;
-    if (have && lane == 0) ntk = atomicAdd(my_counter, 1u);  // next ticket
-    // the pending tile's look-back window (lane i: tile pt-1-i), fetched now and
+    if (FC_ABL & 512) ntk = tk + tk_step;
+    else if (have && lane == 0) ntk = atomicAdd(my_counter, 1u);  // next ticket
+    // the pending tile's look-back window (lane i: tile pt-64+i), fetched now and
     // used after this tile's work
     uint64_t pw1 = kFlagPre, pw2 = kFlagPre;
-    if (pv && pt > lane) {
-      const uint64_t* sp = a.status + 2 * ((int64_t)pc * a.T + pt - 1 - lane);
+    if (!(FC_ABL & 16) && pv && pt + lane >= 64) {
+      const uint64_t* sp = a.status + 2 * ((int64_t)pc * a.T + pt - 64 + lane);
       pw1 = ld_agent(sp);
       pw2 = ld_agent(sp + 1);
     }
@@ -916,7 +1026,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
     if (have) {
       uint32_t* win = wins[buf];
       // tickets interleave clients (tile-major) so each client has few tiles in flight
-      const int32_t t = (int32_t)(ticket / (uint32_t)a.nclients);
+      const int32_t t = (int32_t)div_clients(a, ticket);
       const int32_t c = (int32_t)(ticket - (uint32_t)t * (uint32_t)a.nclients);
       const int64_t tile_base = (int64_t)t * kTE;
       const bool full = tile_base + kTE <= P;
@@ -926,7 +1036,10 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
 #pragma unroll
       for (int j = 0; j < kChunks; ++j) {
         const int64_t e0 = tile_base + 256 * j + 4 * lane;
-        if (full) {
+        if (FC_ABL & 64) {
+          raw[j][0] = (uint32_t)e0 * 2654435761u; raw[j][1] = raw[j][0] ^ 0x9E3779B9u;
+          raw[j][2] = raw[j][0] + 12345u; raw[j][3] = raw[j][1] * 3u;
+        } else if (full) {
           const uint4 v = *(const uint4*)(cp.x + e0);
           raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
         } else {
@@ -934,83 +1047,76 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
           for (int k = 0; k < 4; ++k) raw[j][k] = (e0 + k < P) ? cp.x[e0 + k] : 0u;
         }
       }
-      // ---- A: quantise + chunk-local codes ----
-      ChunkCode cc[kChunks];
+      // ---- A-D, streamed one chunk (4 elements per lane) at a time: quantise
+      //      + chunk-local code, last nonzero before the chunk (max-scan over
+      //      (chunk, lane) order), prepend its first run code, body-relative
+      //      offset (sum-scan), emit into the window.  Registers stay per-chunk.
       float dist = 0.0f;
       int32_t nnz = 0;
+      int32_t carry = -1, wfirst = 0x7FFFFFFF;
+      uint64_t lngmask = 0;
+      uint32_t body = 0;
       {
         const ClientQ cq = client_q_of(cp, pre);
   #pragma unroll
         for (int j = 0; j < kChunks; ++j) {
           const int32_t rel0 = 256 * j + 4 * lane;
+          ChunkCode cc;
           if (INT_IN || (FC_ABL & 8)) {
             int32_t q4[4];
   #pragma unroll
             for (int k = 0; k < 4; ++k) q4[k] = (FC_ABL & 8) ? (int32_t)(raw[j][k] >> 29) - 3 : (int32_t)raw[j][k];
   #pragma unroll
             for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
-            cc[j] = chunk_local(q4, rel0);
+            if (FC_ABL & 2048) {
+              cc.acc = q4[0]; cc.len = q4[1] & 15; cc.lng = 0; cc.first = rel0; cc.last = rel0 + 3;
+            } else {
+              cc = chunk_local(q4, rel0);
+            }
           } else {
             const uint32_t g = (uint32_t)((tile_base + rel0) >> 2);
             if (MODE == FC_DITHERED && !full)
-              cc[j] = quant_code_fast<MODE, RCP, true>(cq, g, raw[j], rel0, dist, nnz,
-                                                       (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - rel0)));
+              cc = quant_code_fast<MODE, RCP, PRE, true>(cq, g, raw[j], rel0, dist, nnz,
+                                                    (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - rel0)));
             else
-              cc[j] = quant_code_fast<MODE, RCP>(cq, g, raw[j], rel0, dist, nnz);
+              cc = quant_code_fast<MODE, RCP, PRE>(cq, g, raw[j], rel0, dist, nnz);
           }
-          __builtin_amdgcn_sched_barrier(0);  // one chunk at a time: bounded mask/VGPR pressure
+          wfirst = min(wfirst, cc.first >= 0 ? cc.first : 0x7FFFFFFF);
+          int32_t prev;
+          uint32_t off;
+          if (FC_ABL & 128) {
+            prev = cc.last - 4;
+            carry = max(carry, cc.last);
+            chunk_prepend(cc, prev);
+            lngmask |= __ballot(cc.lng != 0);
+            off = 16 * lane + 1024 * j;
+            body += 1024;
+          } else {
+            const int32_t im = dpp_incl_max(cc.last);
+            prev = max(dpp_shr1(im, -1), carry);
+            carry = max(carry, lane63(im));
+            chunk_prepend(cc, prev);
+            lngmask |= __ballot(cc.lng != 0);
+            const uint32_t is = dpp_incl_sum(cc.len);
+            off = body + is - cc.len;
+            body += (uint32_t)lane63((int32_t)is);
+          }
+          // codes past the window land in the guard words (the tile is then slow)
+          if (FC_ABL & 1) asm volatile("" :: "v"((uint32_t)cc.acc), "v"(off));
+          else emit64(win, cc.acc, cc.len, kPre + off);
+          FC_CHUNK_BARRIER;
         }
       }
       STAMP(1);
-
-      // ---- B: last nonzero before each chunk (4 interleaved max-scans over
-      //      (chunk, lane) order), then the chunks' run-code prepends ----
-      int32_t carry = -1, wfirst = 0x7FFFFFFF;
-      uint32_t lng = 0;
-      {
-        int32_t im[kChunks];
-  #pragma unroll
-        for (int j = 0; j < kChunks; ++j) im[j] = cc[j].last;
-        dpp_incl_max4(im);
-  #pragma unroll
-        for (int j = 0; j < kChunks; ++j) {
-          const int32_t prev = max(dpp_shr1(im[j], -1), carry);
-          carry = max(carry, lane63(im[j]));
-          wfirst = min(wfirst, cc[j].first >= 0 ? cc[j].first : 0x7FFFFFFF);
-          chunk_prepend(cc[j], prev);
-          lng |= cc[j].lng;
-        }
-      }
-      // ---- C: body-relative offsets (two packed 16-bit sum-scans) ----
-      uint32_t off[kChunks];
-      uint32_t body;
-      {
-        uint32_t s2[2] = {cc[0].len | (cc[1].len << 16), cc[2].len | (cc[3].len << 16)};
-        dpp_incl_sum2(s2);
-        const uint32_t t0 = (uint32_t)lane63((int32_t)s2[0]), t1 = (uint32_t)lane63((int32_t)s2[1]);
-        const uint32_t b1 = t0 & 0xFFFFu, b2 = b1 + (t0 >> 16), b3 = b2 + (t1 & 0xFFFFu);
-        off[0] = (s2[0] & 0xFFFFu) - cc[0].len;
-        off[1] = b1 + (s2[0] >> 16) - cc[1].len;
-        off[2] = b2 + (s2[1] & 0xFFFFu) - cc[2].len;
-        off[3] = b3 + (s2[1] >> 16) - cc[3].len;
-        body = b3 + (t1 >> 16);
-      }
-      // fast path: whole tile inside the tensor (or int input), no long chunk, and
-      // prefix + body + trailing code + one funnel word fit the wave's window
-      const bool fast = __ballot(lng != 0) == 0 && kPre + body + 96u <= 32u * kWinWords;
-      // ---- D: emit (body-relative) ----
-      if (FC_ABL & 1) {
-        asm volatile("" :: "v"((uint32_t)cc[0].acc), "v"((uint32_t)cc[3].acc), "v"(off[0]), "v"(off[3]));
-      } else {
-  #pragma unroll
-        for (int j = 0; j < kChunks; ++j) emit64(win, cc[j].acc, cc[j].len, kPre + off[j]);
-      }
+      // fast path: no long chunk, and prefix + body + trailing code + one funnel
+      // word fit the wave's window
+      const bool fast = lngmask == 0 && kPre + body + 96u <= 32u * kWinWords;
       STAMP(2);
 
       const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;
       const int32_t tile_last = carry;
-      const int32_t tile_first = wave_min_i(wfirst);
-      if (fast) {
+      const int32_t tile_first = (FC_ABL & 32) ? lane63(wfirst) : wave_min_i(wfirst);
+      if (fast && !(FC_ABL & 32)) {
         const float d = wave_sum_f(dist);
         const int32_t n = wave_sum_i(nnz);
         if (lane == 0) {
@@ -1019,6 +1125,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         }
       }
       next = shard + a.nshards * uniform(ntk);
+      if (FC_ABL & 512) tk = ntk;
       STAMP(3);
       uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t);
       if (!fast) {
@@ -1080,7 +1187,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         excl.has_nz = 1;
         excl.first = excl.last = -1;
       } else {
-        excl = lookback(a.status + 2 * (int64_t)pc * a.T, pt, lane, a.spin_err, slow, true, pw1, pw2);
+        excl = lookback_vec(a.status + 2 * (int64_t)pc * a.T, pt, lane, a.spin_err, slow, pw1, pw2);
       }
       if (slow) {
         if (lane == 0) {
@@ -1130,12 +1237,14 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         const uint64_t w0 = excl.body >> 5;
         if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&a.overflow[pc], 1u);
         const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
+        if (!(FC_ABL & 1024))
         for (uint32_t k = lane; k < nwords_owned; k += kEncThreads) {
           const uint32_t wv32 = win_bits32(win, s0 + 32 * k);
           if (FC_ABL & 2) asm volatile("" :: "v"(wv32));
           else if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
         }
         const uint32_t nt = min((uint32_t)kWinWords, (kPre + pbody + trail_len + 31) / 32 + 1);
+        if (!(FC_ABL & 1024))
         for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
       }
     }
@@ -1853,12 +1962,23 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   a.rcp = pow2 ? 1.0f / step : 0.0f;
   void (*kern)(EncodeArgs) = nullptr;
   void (*exact)(EncodeArgs) = nullptr;
-#define FC_PICK(M, I, R) (kern = k_encode<M, I, R>, exact = k_encode_exact<M, I, R>)
-  if (int_in) FC_PICK(FC_UNIFORM, true, false);
-  else if (mode == FC_UNIFORM) pow2 ? FC_PICK(FC_UNIFORM, false, true) : FC_PICK(FC_UNIFORM, false, false);
-  else if (mode == FC_STOCHASTIC) pow2 ? FC_PICK(FC_STOCHASTIC, false, true) : FC_PICK(FC_STOCHASTIC, false, false);
-  else pow2 ? FC_PICK(FC_DITHERED, false, true) : FC_PICK(FC_DITHERED, false, false);
+  const bool pre = !int_in && prescale != nullptr;
+#define FC_PICK(M, I, R, Q) (kern = k_encode<M, I, R, Q>, exact = k_encode_exact<M, I, R>)
+#define FC_PICK2(M, R) (pre ? FC_PICK(M, false, R, true) : FC_PICK(M, false, R, false))
+  if (int_in) FC_PICK(FC_UNIFORM, true, false, false);
+  else if (mode == FC_UNIFORM) pow2 ? FC_PICK2(FC_UNIFORM, true) : FC_PICK2(FC_UNIFORM, false);
+  else if (mode == FC_STOCHASTIC) pow2 ? FC_PICK2(FC_STOCHASTIC, true) : FC_PICK2(FC_STOCHASTIC, false);
+  else pow2 ? FC_PICK2(FC_DITHERED, true) : FC_PICK2(FC_DITHERED, false);
+#undef FC_PICK2
 #undef FC_PICK
+  {  // ticket -> (tile, client) by multiply-high
+    const uint32_t d = (uint32_t)nclients;
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) ++l;
+    a.div_l = l;
+    a.div_m = l == 0 ? 0u : (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  }
+  if ((uint64_t)nclients * (uint64_t)T >= (1ull << 32)) return fail(-1, "too many tiles (nclients x tiles >= 2^32)");
   // Persistent grid no larger than what is co-resident (every ticket stream has a
   // running workgroup); few clients: cap the tiles in flight per client so the
   // look-back windows stay short.
@@ -1888,9 +2008,9 @@ const char* fc_last_error(void) { return g_err.c_str(); }
 const char* fc_version(void) { return "fedcodec 0.1 gfx950"; }
 #ifdef FC_STAMPS
 int fc_debug_stamps(unsigned long long* host8, int reset) {
-  if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

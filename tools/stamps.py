@@ -27,7 +27,7 @@ rows = [pool[c % 4] for c in range(C)]
 ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
 seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
 batch = codec.EncodedBatch(P, C, [P + 1024] * C, dev)
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 16)()
 for it in range(3):
   if HAVE:
     lib.fc_debug_stamps(buf, 1)
@@ -48,3 +48,6 @@ tot = sum(buf[i] for i in range(len(names)))
 print("encode %.2f ms, %d tiles, %.0f cycles/tile total (memtime units)" % (dt * 1e3, tiles, tot / tiles))
 for i, n in enumerate(names):
   print("  %-22s %8.0f  %5.1f%%" % (n, buf[i] / tiles, 100.0 * buf[i] / tot))
+cn = {8: "vec lookbacks", 9: "re-polls", 10: "no prefix in 64", 11: "short-body fallback", 12: "predecessor prefix", 13: "sum fold depth"}
+for i, n in cn.items():
+  print("  %-22s %12d  (%.3f per tile)" % (n, buf[i], buf[i] / tiles))
