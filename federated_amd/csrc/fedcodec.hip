@@ -1605,82 +1605,148 @@ struct SegReader {
   }
 };
 
-__device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
-                                               uint64_t b1, int32_t rel, int32_t* my, int32_t* err) {
-  SegReader r;
-  r.init(base, cap, b0);
-  uint64_t pos = b0;
-  uint32_t bad = 0;
-  while (pos < b1) {
-    const uint32_t top = (uint32_t)(r.win >> 32);
+// Decode table: the next 12 window bits -> up to two complete codes.
+//   [3:0] L1  bits of code 1 (0: code 1 is longer than 12 bits)
+//   [7:4] L   bits of both codes (= L1 when only one fits)
+//   [12:8] d1   [18:13] v1 + 32   [23:19] d2   [29:24] v2 + 32   [31:30] n codes
+constexpr int kLutBits = 12;
+constexpr int kLutSize = 1 << kLutBits;
+
+__device__ __forceinline__ uint32_t lut_entry(uint32_t x) {
+  uint32_t top = x << (32 - kLutBits);
+  uint32_t used = 0, n = 0, e = 0;
+  for (int c = 0; c < 2; ++c) {
     const uint32_t z1 = (uint32_t)__clz(top);
-    const uint32_t sa = 30u - 2u * z1;        // sign-bit position
-    const uint32_t rest = top << (32u - sa);  // bits after the sign bit
+    if (z1 > 4) break;
+    const uint32_t sa = 30u - 2u * z1;
+    const uint32_t rest = top << (32u - sa);
     const uint32_t z2 = (uint32_t)__clz(rest);
-    uint32_t L = 2u * (z1 + z2) + 3u;
-    uint32_t d = top >> (sa + 1u);
+    if (z2 > 4) break;
+    const uint32_t L = 2u * (z1 + z2) + 3u;
+    if (used + L > (uint32_t)kLutBits) break;
+    const uint32_t d = top >> (sa + 1u);
     const uint32_t m = rest >> (31u - 2u * z2);
-    int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
-    if (L <= 32u) {
-      r.win <<= L;
-      r.nwin -= (int32_t)L;
-      if (r.nwin <= 32) {
-        r.win |= (uint64_t)r.pop32() << (32 - r.nwin);
-        r.nwin += 32;
-      }
-    } else {  // rare: a code longer than 32 bits (or a malformed one)
-      const CodeVal cv = slow_code(base, cap, pos);
-      if (cv.L == 0) {
-        bad = 1;
-        break;
-      }
-      L = cv.L;
-      d = cv.d;
-      v = cv.v;
-      r.init(base, cap, pos + L);
-    }
-    pos += L;
-    rel += (int32_t)d;
-    bad |= (uint32_t)rel >= (uint32_t)kTE;
-    atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v);
+    const int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
+    used += L;
+    if (c == 0) e |= L | (d << 8) | ((uint32_t)(v + 32) << 13);
+    else e |= (d << 19) | ((uint32_t)(v + 32) << 24);
+    ++n;
+    top <<= L;
   }
-  if (bad || pos != b1) atomicOr(err, 1);
+  return e | (used << 4) | (n << 30);
 }
 
+// One segment = one client's code for one 1024-element tile: bits [b0, b1),
+// previous nonzero at tile-relative position rel.  Each step looks up the next
+// 12 window bits (one or two short codes); a code longer than 12 bits is
+// decoded arithmetically from the top 32 window bits, one longer than 32 bits
+// by slow_code (the reader then restarts after it).
+__device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
+                                               uint64_t b1, int32_t rel, int32_t* my,
+                                               const uint32_t* lut, int32_t* err) {
+  SegReader r;
+  r.init(base, cap, b0);
+  int64_t rem = (int64_t)(b1 - b0);
+  uint32_t bad = 0;
+  while (rem > 0) {
+    const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+    uint32_t L;
+    if (e & 15u) {
+      const uint32_t L1 = e & 15u, L2 = (e >> 4) & 15u;
+      const bool two = (e >> 30) == 2u && (int64_t)L2 <= rem;
+      L = two ? L2 : L1;
+      const int32_t rel1 = rel + (int32_t)((e >> 8) & 31u);
+      const int32_t rel2 = rel1 + (int32_t)((e >> 19) & 31u);
+      const int32_t v1 = (int32_t)((e >> 13) & 63u) - 32;
+      const int32_t v2 = two ? (int32_t)((e >> 24) & 63u) - 32 : 0;
+      rel = two ? rel2 : rel1;  // (a second code past the segment end is not ours)
+      bad |= (uint32_t)rel >= (uint32_t)kTE;
+      atomicAdd(&my[min((uint32_t)rel1, (uint32_t)kTE - 1)], v1);
+      atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v2);
+      r.win <<= L;
+      r.nwin -= (int32_t)L;
+    } else {
+      const uint32_t top = (uint32_t)(r.win >> 32);
+      const uint32_t z1 = (uint32_t)__clz(top);
+      const uint32_t sa = 30u - 2u * z1;        // sign-bit position
+      const uint32_t rest = top << (32u - sa);  // bits after the sign bit
+      const uint32_t z2 = (uint32_t)__clz(rest);
+      L = 2u * (z1 + z2) + 3u;
+      uint32_t d = top >> (sa + 1u);
+      const uint32_t m = rest >> (31u - 2u * z2);
+      int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
+      if (L <= 32u) {
+        r.win <<= L;
+        r.nwin -= (int32_t)L;
+      } else {  // a code longer than 32 bits (or a malformed one)
+        const uint64_t pos = b1 - (uint64_t)rem;
+        const CodeVal cv = slow_code(base, cap, pos);
+        if (cv.L == 0) {
+          bad = 1;
+          break;
+        }
+        L = cv.L;
+        d = cv.d;
+        v = cv.v;
+        r.init(base, cap, pos + L);
+      }
+      rel += (int32_t)d;
+      bad |= (uint32_t)rel >= (uint32_t)kTE;
+      atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v);
+    }
+    if (r.nwin <= 32) {
+      r.win |= (uint64_t)r.pop32() << (32 - r.nwin);
+      r.nwin += 32;
+    }
+    rem -= (int64_t)L;
+  }
+  if (bad || rem != 0) atomicOr(err, 1);
+}
+
+// Persistent: each workgroup builds the decode table once, then walks tiles
+// (tiles_per_wg at a time) with one lane per client segment, accumulating the
+// clients' values in LDS and writing the tile's sum / dequantised values.
 __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
-  extern __shared__ int32_t acc[];  // [tiles_per_wg][kTE]
+  extern __shared__ int32_t smem[];  // [kLutSize] table, then [tiles_per_wg][kTE] sums
+  uint32_t* lut = (uint32_t*)smem;
+  int32_t* acc = smem + kLutSize;
   const int tid = threadIdx.x;
   const int tiles_per_wg = kThreads / a.lanes_per_tile;
-  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_wg;
-  for (int i = tid; i < tiles_per_wg * kTE; i += kThreads) acc[i] = 0;
-  __syncthreads();
+  for (int i = tid; i < kLutSize; i += kThreads) lut[i] = lut_entry((uint32_t)i);
   const int sub = tid / a.lanes_per_tile;
   const int l = tid - sub * a.lanes_per_tile;
-  const int64_t t = t0 + sub;
   int32_t* my = acc + sub * kTE;
-  if (t < a.T) {
-    const int64_t tile_base = t * kTE;
-    for (int c = l; c < a.nclients; c += a.lanes_per_tile) {
-      const int64_t ib = (int64_t)c * (a.T + 1) + t;
-      const uint64_t e0 = a.idx[ib], e1 = a.idx[ib + 1];
-      const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
-      if (bend <= bstart) continue;
-      const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
-      decode_segment(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart, bend, rel, my, a.err);
+  const int64_t ngroups = (a.T + tiles_per_wg - 1) / tiles_per_wg;
+  for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int64_t t0 = grp * tiles_per_wg;
+    for (int i = tid; i < tiles_per_wg * kTE; i += kThreads) acc[i] = 0;
+    __syncthreads();
+    const int64_t t = t0 + sub;
+    if (t < a.T) {
+      const int64_t tile_base = t * kTE;
+      for (int c = l; c < a.nclients; c += a.lanes_per_tile) {
+        const int64_t ib = (int64_t)c * (a.T + 1) + t;
+        const uint64_t e0 = a.idx[ib], e1 = a.idx[ib + 1];
+        const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
+        if (bend <= bstart) continue;
+        const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
+        decode_segment(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart, bend, rel, my, lut, a.err);
+      }
     }
-  }
-  __syncthreads();
-  for (int i = tid; i < tiles_per_wg * kTE; i += kThreads) {
-    const int64_t e = t0 * kTE + i;
-    if (e >= a.P) break;
-    int32_t v = acc[i];
-    if (a.sum_in) v = (int32_t)((uint32_t)v + (uint32_t)a.sum_in[e]);
-    if (a.sum_out) a.sum_out[e] = v;
-    if (a.out) {
-      float f = (float)v;
-      if (a.noise_sum) f = f + a.noise_sum[e];
-      a.out[e] = f * a.step;
+    __syncthreads();
+    for (int i = tid; i < tiles_per_wg * kTE; i += kThreads) {
+      const int64_t e = t0 * kTE + i;
+      if (e >= a.P) break;
+      int32_t v = acc[i];
+      if (a.sum_in) v = (int32_t)((uint32_t)v + (uint32_t)a.sum_in[e]);
+      if (a.sum_out) a.sum_out[e] = v;
+      if (a.out) {
+        float f = (float)v;
+        if (a.noise_sum) f = f + a.noise_sum[e];
+        a.out[e] = f * a.step;
+      }
     }
+    __syncthreads();
   }
 }
 
@@ -2083,10 +2149,17 @@ int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off, c
   a.noise_sum = noise_sum;
   a.err = err;
   const int tpw = kThreads / lpt;
-  const dim3 grid((unsigned)((a.T + tpw - 1) / tpw));
+  const size_t lds = (size_t)kLutSize * 4 + (size_t)tpw * kTE * sizeof(int32_t);
+  int dev = 0, ncu = 256, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode, kThreads, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  const int64_t ngroups = (a.T + tpw - 1) / tpw;
+  const dim3 grid((unsigned)std::min<int64_t>(ngroups, (int64_t)ncu * per_cu));
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(err, 0, sizeof(int32_t), s) != hipSuccess) return fail(-10, "memset err");
-  hipLaunchKernelGGL(k_decode, grid, dim3(kThreads), (size_t)tpw * kTE * sizeof(int32_t), s, a);
+  hipLaunchKernelGGL(k_decode, grid, dim3(kThreads), lds, s, a);
   return check_launch("k_decode");
 }
 
