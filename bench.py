@@ -107,6 +107,27 @@ def cpu_baseline(args):
                         n, P, args.mode, args.step_size, cores, t)}
 
 
+def measured_traffic(args, C):
+  """Per-launch HBM bytes of k_encode from the latest committed PMC profile of this exact
+  workload (profiles/*/traffic.json, written from tools/profile_bench.sh's FETCH_SIZE and
+  WRITE_SIZE passes with the gfx950 correction), else None."""
+  import glob  # pylint: disable=g-import-not-at-top
+  best = None
+  for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
+    try:
+      with open(f) as fh:
+        d = json.load(fh)
+    except (OSError, ValueError):
+      continue
+    cfg = d.get("config", {})
+    if (cfg.get("clients"), cfg.get("P"), cfg.get("mode"), cfg.get("step")) == (C, args.P, args.mode,
+                                                                               args.step_size):
+      best = (f, d)
+  if best is None:
+    return None, None
+  return best[1]["k_encode"]["hbm_bytes_corrected"], os.path.relpath(best[0], ROOT)
+
+
 def main():
   args = parse()
   rank, world = setup_dist(args)
@@ -202,6 +223,7 @@ def main():
   step_bytes = Cg * 4.0 * P + 2 * S + 12.0 * P  # BASELINE.md B_alg per GPU
 
   result = None
+  traffic, traffic_src = measured_traffic(args, C) if world == 1 else (None, None)
   if rank == 0:
     value = C * P * 4.0 / t_step / 2**30
     result = {
@@ -228,7 +250,8 @@ def main():
                      "achieved": round(enc_bytes / t_enc / 1e9, 1),
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": round(enc_bytes / t_enc / HBM_PEAK, 4),
-                     "traffic": None,
+                     "traffic": round(traffic) if traffic else None,
+                     "traffic_source": traffic_src,
                      "alg_bytes_per_launch": enc_bytes, "launch_ms": round(t_enc * 1e3, 3)},
         "decode": {"kernel": "k_decode", "launch_ms": round(t_dec * 1e3, 3),
                    "alg_GBps": round(dec_bytes / t_dec / 1e9, 1)},

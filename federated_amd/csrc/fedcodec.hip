@@ -2156,7 +2156,9 @@ int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off, c
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode, kThreads, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
   const int64_t ngroups = (a.T + tpw - 1) / tpw;
-  const dim3 grid((unsigned)std::min<int64_t>(ngroups, (int64_t)ncu * per_cu));
+  int64_t max_grid = (int64_t)ncu * per_cu;
+  if (const char* g = getenv("FEDCODEC_DEC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
+  const dim3 grid((unsigned)std::min<int64_t>(ngroups, max_grid));
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(err, 0, sizeof(int32_t), s) != hipSuccess) return fail(-10, "memset err");
   hipLaunchKernelGGL(k_decode, grid, dim3(kThreads), lds, s, a);
