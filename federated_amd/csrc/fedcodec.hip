@@ -609,7 +609,8 @@ __device__ __forceinline__ ChunkCode chunk_local(const int32_t (&q4)[4], int32_t
 template <int MODE, bool RCP, bool PRE, bool MASK = false>
 __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t g,
                                                      const uint32_t (&r4)[4], int32_t rel0,
-                                                     float& dist, int32_t& nnz, int32_t nvalid = 4) {
+                                                     float& dist, int32_t& nnz, const uint32_t* clut,
+                                                     int32_t nvalid = 4) {
   uint4 rb = make_uint4(0, 0, 0, 0);
   if (MODE != FC_UNIFORM) rb = philox_group(cq.key, g);
   const uint32_t rbits[4] = {rb.x, rb.y, rb.z, rb.w};
@@ -651,6 +652,20 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
   ChunkCode r;
   r.acc = 0;
   r.len = 0;
+  // small values across the wave (|q| <= 31, the common case): one table read per element
+  bool big = false;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) big |= !(fabsf(q[k]) <= 31.0f);
+  if (__ballot(big) == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t qi = (uint32_t)(int32_t)q[k];
+      const uint32_t e = clut[(dv[k] << 6) | (qi & 63u)];  // zero -> empty code
+      const uint32_t L = e >> 16;
+      r.acc = k == 0 ? (uint64_t)(e & 0xFFFFu) : ((r.acc << L) | (e & 0xFFFFu));
+      r.len += L;
+    }
+  } else {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t m = (uint32_t)fabsf(q[k]);
@@ -664,10 +679,29 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
     r.acc = k == 0 ? (uint64_t)code : ((r.acc << L) | code);
     r.len += L;
   }
+  }
   r.first = nz[0] ? rel0 : (nz[1] ? rel0 + 1 : (nz[2] ? rel0 + 2 : (nz[3] ? rel0 + 3 : -1)));
   r.last = nz[3] ? rel0 + 3 : (nz[2] ? rel0 + 2 : (nz[1] ? rel0 + 1 : (nz[0] ? rel0 : -1)));
   r.lng = (bad || r.len > 64u) ? 1u : 0u;
   return r;
+}
+
+// Chunk code table: entry (ds << 6) | (q & 63) for |q| <= 31 is the code of a
+// nonzero q whose in-chunk run value is ds (0: the chunk's first nonzero, whose
+// run code is prepended later) -- [15:0] code bits, [31:16] length; q = 0 -> 0.
+constexpr int kCodeLut = 256;
+__device__ __forceinline__ uint32_t code_lut_entry(uint32_t i) {
+  const uint32_t ds = i >> 6;
+  const int32_t q = ((int32_t)(i << 26)) >> 26;  // sign-extend 6 bits
+  if (q == 0 || ds > 3) return 0u;
+  const uint32_t m = (uint32_t)(q < 0 ? -q : q);
+  const uint32_t ml = glen(m);
+  uint32_t code = ((uint32_t)(q > 0) << ml) | m, L = 1u + ml;
+  if (ds) {
+    code |= ds << L;
+    L += glen(ds);
+  }
+  return code | (L << 16);
 }
 
 // Prepend the run code of the chunk's first nonzero once the last nonzero
@@ -980,7 +1014,9 @@ __device__ __forceinline__ void slow_emit(const EncodeArgs& a, const ClientQ& cq
 template <int MODE, bool INT_IN, bool RCP, bool PRE>
 __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs a) {
   __shared__ uint32_t wins[2][kWinWords + 3];  // double-buffered; + guard words
+  __shared__ uint32_t clut[kCodeLut];
   const int lane = threadIdx.x;
+  for (int i = lane; i < kCodeLut; i += kEncThreads) clut[i] = code_lut_entry((uint32_t)i);
   const uint32_t total_tiles = (uint32_t)a.nclients * (uint32_t)a.T;
   const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
   constexpr bool pre = PRE;
@@ -1076,10 +1112,10 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
           } else {
             const uint32_t g = (uint32_t)((tile_base + rel0) >> 2);
             if (MODE == FC_DITHERED && !full)
-              cc = quant_code_fast<MODE, RCP, PRE, true>(cq, g, raw[j], rel0, dist, nnz,
+              cc = quant_code_fast<MODE, RCP, PRE, true>(cq, g, raw[j], rel0, dist, nnz, clut,
                                                     (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - rel0)));
             else
-              cc = quant_code_fast<MODE, RCP, PRE>(cq, g, raw[j], rel0, dist, nnz);
+              cc = quant_code_fast<MODE, RCP, PRE>(cq, g, raw[j], rel0, dist, nnz, clut);
           }
           wfirst = min(wfirst, cc.first >= 0 ? cc.first : 0x7FFFFFFF);
           int32_t prev;
@@ -1567,6 +1603,9 @@ __device__ __noinline__ CodeVal slow_code(const uint8_t* base, int64_t cap, uint
 // 16-byte block already in flight.  Codes that fit the top 32 window bits are
 // decoded branch-free; longer ones go through slow_code and the reader
 // restarts after them.
+#ifndef FC_DEC_ABL
+#define FC_DEC_ABL 0  // decoder ablation bits (diagnostics only): 1 no LDS sums, 2 no table reads
+#endif
 #ifndef FC_DEC_BLOCKS
 #define FC_DEC_BLOCKS 1
 #endif
@@ -1672,8 +1711,16 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
   r.init(base, cap, b0);
   int64_t rem = (int64_t)(b1 - b0);
   uint32_t bad = 0;
+  int32_t fake = 0;
   while (rem > 0) {
-    const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+    uint32_t e;
+    if (FC_DEC_ABL & 2) {  // diagnostic: no table read
+      const uint32_t x = (uint32_t)(r.win >> (64 - kLutBits));
+      e = 5u | (10u << 4) | (1u << 8) | (33u << 13) | (1u << 19) | (31u << 24) | (2u << 30);
+      e ^= (x & 1u) << 13;
+    } else {
+      e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+    }
     uint32_t L;
     if (e & 15u) {
       const uint32_t L1 = e & 15u, L2 = (e >> 4) & 15u;
@@ -1685,8 +1732,12 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       const int32_t v2 = two ? (int32_t)((e >> 24) & 63u) - 32 : 0;
       rel = two ? rel2 : rel1;  // (a second code past the segment end is not ours)
       bad |= (uint32_t)rel >= (uint32_t)kTE;
-      atomicAdd(&my[min((uint32_t)rel1, (uint32_t)kTE - 1)], v1);
-      atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v2);
+      if (FC_DEC_ABL & 1) {  // diagnostic: no LDS accumulation
+        fake += v1 * rel1 + v2 * rel;
+      } else {
+        atomicAdd(&my[min((uint32_t)rel1, (uint32_t)kTE - 1)], v1);
+        atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v2);
+      }
       r.win <<= L;
       r.nwin -= (int32_t)L;
     } else {
@@ -1724,6 +1775,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     }
     rem -= (int64_t)L;
   }
+  if (FC_DEC_ABL & 1) bad |= fake == 123456789;
   if (bad || rem != 0) atomicOr(err, 1);
 }
 
