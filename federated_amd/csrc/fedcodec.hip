@@ -1704,40 +1704,41 @@ __device__ __forceinline__ uint32_t lut_entry(uint32_t x) {
 // 12 window bits (one or two short codes); a code longer than 12 bits is
 // decoded arithmetically from the top 32 window bits, one longer than 32 bits
 // by slow_code (the reader then restarts after it).
+// One table step: up to two codes from the next 12 window bits (caller checked
+// e & 15 != 0, i.e. the first code fits).  Returns the bits consumed.
+__device__ __forceinline__ uint32_t table_step(uint32_t e, int32_t rem, int32_t& rel, int32_t* my,
+                                               uint32_t& bad) {
+  const uint32_t L1 = e & 15u, L2 = (e >> 4) & 15u;
+  const bool two = (e >> 30) == 2u && (int32_t)L2 <= rem;  // a second code past the segment is not ours
+  const int32_t rel1 = rel + (int32_t)((e >> 8) & 31u);
+  const int32_t rel2 = rel1 + (int32_t)((e >> 19) & 31u);
+  const int32_t v1 = (int32_t)((e >> 13) & 63u) - 32;
+  const int32_t v2 = two ? (int32_t)((e >> 24) & 63u) - 32 : 0;
+  rel = two ? rel2 : rel1;
+  bad |= (uint32_t)rel >= (uint32_t)kTE;
+  atomicAdd(&my[min((uint32_t)rel1, (uint32_t)kTE - 1)], v1);
+  atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v2);
+  return two ? L2 : L1;
+}
+
+// One segment = one client's code for one 1024-element tile: bits [b0, b1),
+// previous nonzero at tile-relative position rel.  Each iteration makes two
+// steps and one window refill: step A looks up the next 12 window bits (one or
+// two short codes) or decodes a longer code arithmetically from the top 32 bits
+// (longer than 32 bits: slow_code, then the reader restarts); step B is a
+// table step when >= 12 bits remain in the window.  Segments are < 2^31 bits.
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
                                                uint64_t b1, int32_t rel, int32_t* my,
                                                const uint32_t* lut, int32_t* err) {
   SegReader r;
   r.init(base, cap, b0);
-  int64_t rem = (int64_t)(b1 - b0);
+  int32_t rem = (int32_t)(b1 - b0);
   uint32_t bad = 0;
-  int32_t fake = 0;
   while (rem > 0) {
-    uint32_t e;
-    if (FC_DEC_ABL & 2) {  // diagnostic: no table read
-      const uint32_t x = (uint32_t)(r.win >> (64 - kLutBits));
-      e = 5u | (10u << 4) | (1u << 8) | (33u << 13) | (1u << 19) | (31u << 24) | (2u << 30);
-      e ^= (x & 1u) << 13;
-    } else {
-      e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
-    }
+    uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
     uint32_t L;
     if (e & 15u) {
-      const uint32_t L1 = e & 15u, L2 = (e >> 4) & 15u;
-      const bool two = (e >> 30) == 2u && (int64_t)L2 <= rem;
-      L = two ? L2 : L1;
-      const int32_t rel1 = rel + (int32_t)((e >> 8) & 31u);
-      const int32_t rel2 = rel1 + (int32_t)((e >> 19) & 31u);
-      const int32_t v1 = (int32_t)((e >> 13) & 63u) - 32;
-      const int32_t v2 = two ? (int32_t)((e >> 24) & 63u) - 32 : 0;
-      rel = two ? rel2 : rel1;  // (a second code past the segment end is not ours)
-      bad |= (uint32_t)rel >= (uint32_t)kTE;
-      if (FC_DEC_ABL & 1) {  // diagnostic: no LDS accumulation
-        fake += v1 * rel1 + v2 * rel;
-      } else {
-        atomicAdd(&my[min((uint32_t)rel1, (uint32_t)kTE - 1)], v1);
-        atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v2);
-      }
+      L = table_step(e, rem, rel, my, bad);
       r.win <<= L;
       r.nwin -= (int32_t)L;
     } else {
@@ -1769,13 +1770,19 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       bad |= (uint32_t)rel >= (uint32_t)kTE;
       atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v);
     }
+    rem -= (int32_t)L;
+    e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+    if (rem > 0 && r.nwin >= kLutBits && (e & 15u)) {
+      L = table_step(e, rem, rel, my, bad);
+      r.win <<= L;
+      r.nwin -= (int32_t)L;
+      rem -= (int32_t)L;
+    }
     if (r.nwin <= 32) {
       r.win |= (uint64_t)r.pop32() << (32 - r.nwin);
       r.nwin += 32;
     }
-    rem -= (int64_t)L;
   }
-  if (FC_DEC_ABL & 1) bad |= fake == 123456789;
   if (bad || rem != 0) atomicOr(err, 1);
 }
 
