@@ -639,7 +639,7 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
     dist = (!MASK || k < nvalid) ? fmaf(dd, dd, dist) : dist;
     q[k] = r;
     nz[k] = r != 0.0f;
-    nnz += nz[k] ? 1 : 0;
+    nnz += (int32_t)__popcll(__ballot(nz[k]));  // wave total, scalar unit
   }
   // run code (value dv in rl bits) before element k, from the previous nonzero in the chunk
   const uint32_t dv1 = nz[0] ? 1u : 0u;
@@ -1088,8 +1088,8 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
       //      (chunk, lane) order), prepend its first run code, body-relative
       //      offset (sum-scan), emit into the window.  Registers stay per-chunk.
       float dist = 0.0f;
-      int32_t nnz = 0;
-      int32_t carry = -1, wfirst = 0x7FFFFFFF;
+      int32_t nnz = 0;  // INT_IN: per lane; float input: wave total
+      int32_t carry = -1, wfirst = 0x7FFFFFFF, sfirst = -1;
       uint64_t lngmask = 0;
       uint32_t body = 0;
       {
@@ -1117,7 +1117,12 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
             else
               cc = quant_code_fast<MODE, RCP, PRE>(cq, g, raw[j], rel0, dist, nnz, clut);
           }
-          wfirst = min(wfirst, cc.first >= 0 ? cc.first : 0x7FFFFFFF);
+          if (INT_IN || (FC_ABL & 8)) {
+            wfirst = min(wfirst, cc.first >= 0 ? cc.first : 0x7FFFFFFF);
+          } else if (sfirst < 0) {  // the tile's first nonzero: first chunk with one, lowest lane
+            const uint64_t fm = __ballot(cc.first >= 0);
+            if (fm) sfirst = __builtin_amdgcn_readlane(cc.first, (int)__builtin_ctzll(fm));
+          }
           int32_t prev;
           uint32_t off;
           if (FC_ABL & 128) {
@@ -1151,10 +1156,10 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
 
       const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;
       const int32_t tile_last = carry;
-      const int32_t tile_first = (FC_ABL & 32) ? lane63(wfirst) : wave_min_i(wfirst);
+      const int32_t tile_first = (INT_IN || (FC_ABL & 8)) ? wave_min_i(wfirst) : sfirst;
       if (fast && !(FC_ABL & 32)) {
         const float d = wave_sum_f(dist);
-        const int32_t n = wave_sum_i(nnz);
+        const int32_t n = (INT_IN || (FC_ABL & 8)) ? wave_sum_i(nnz) : nnz;
         if (lane == 0) {
           if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
           if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t] = n;
