@@ -29,7 +29,7 @@
 // Diagnostic ablation bits (performance experiments only; 0 in every real build):
 //   1 skip LDS emission  2 skip stream stores  4 skip look-back  8 skip quantise math
 #ifndef FC_ENC_WAVES
-#define FC_ENC_WAVES 5  // encoder waves per SIMD the register budget is sized for
+#define FC_ENC_WAVES 4  // encoder waves per SIMD the register budget is sized for (LDS: 4 per SIMD)
 #endif
 #ifndef FC_CHUNK_BARRIER
 #define FC_CHUNK_BARRIER __builtin_amdgcn_sched_barrier(0)
@@ -76,6 +76,34 @@ __host__ __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, ui
   }
 }
 
+// Philox4x32-10 with a wave-uniform key (the encoder's per-client key lives in
+// SGPRs): each round's two 3-input xors are one gfx950 v_bitop3_b32 each
+// (truth table 0x96 = a ^ b ^ c), which the compiler does not form by itself.
+__device__ __forceinline__ uint32_t xor3_vvs(uint32_t a, uint32_t b, uint32_t s) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(s));
+  return r;
+}
+// Rounds 0-1 stay plain C: with a lane-varying c0 only, half of their products
+// and xors are wave-uniform and the compiler moves them to the scalar unit.
+__device__ __forceinline__ void philox10_ukey(uint32_t& c0, uint32_t& c1, uint32_t& c2,
+                                              uint32_t& c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t kk0 = __builtin_amdgcn_readfirstlane(k0), kk1 = __builtin_amdgcn_readfirstlane(k1);
+    const uint32_t n0 = r < 2 ? (uint32_t)(p1 >> 32) ^ c1 ^ kk0 : xor3_vvs((uint32_t)(p1 >> 32), c1, kk0);
+    const uint32_t n2 = r < 2 ? (uint32_t)(p0 >> 32) ^ c3 ^ kk1 : xor3_vvs((uint32_t)(p0 >> 32), c3, kk1);
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
 __host__ __device__ __forceinline__ Key4 tf_seed_scramble(int64_t s0, int64_t s1) {
   uint32_t c0 = (uint32_t)(uint64_t)s0, c1 = (uint32_t)((uint64_t)s0 >> 32);
   uint32_t c2 = (uint32_t)(uint64_t)s1, c3 = (uint32_t)((uint64_t)s1 >> 32);
@@ -87,6 +115,13 @@ __host__ __device__ __forceinline__ Key4 tf_seed_scramble(int64_t s0, int64_t s1
 __device__ __forceinline__ uint4 philox_group(const Key4& k, uint32_t g) {
   uint32_t c0 = g, c1 = 0, c2 = k.c2, c3 = k.c3;
   philox10(c0, c1, c2, c3, k.k0, k.k1);
+  return make_uint4(c0, c1, c2, c3);
+}
+
+// Same, for a key that is uniform across the wave (k_encode's per-client key).
+__device__ __forceinline__ uint4 philox_group_u(const Key4& k, uint32_t g) {
+  uint32_t c0 = g, c1 = 0, c2 = k.c2, c3 = k.c3;
+  philox10_ukey(c0, c1, c2, c3, k.k0, k.k1);
   return make_uint4(c0, c1, c2, c3);
 }
 
@@ -600,6 +635,12 @@ __device__ __forceinline__ ChunkCode chunk_local(const int32_t (&q4)[4], int32_t
   return r;
 }
 
+__device__ __forceinline__ float vmax3_abs(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // Fused quantise + chunk-local code of one chunk of 4 in-range float
 // elements (the fast path's inner loop).  The rounded value stays a float (an
 // exact integer when |r| < 8192): m = |r| by one conversion, floor(log2 m) is
@@ -612,11 +653,10 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
                                                      float& dist, int32_t& nnz, const uint32_t* clut,
                                                      int32_t nvalid = 4) {
   uint4 rb = make_uint4(0, 0, 0, 0);
-  if (MODE != FC_UNIFORM) rb = philox_group(cq.key, g);
+  if (MODE != FC_UNIFORM) rb = philox_group_u(cq.key, g);
   const uint32_t rbits[4] = {rb.x, rb.y, rb.z, rb.w};
   float q[4];
   bool nz[4];
-  bool bad = false;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     float xv = __uint_as_float(r4[k]);
@@ -632,7 +672,6 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
       noise = u01(rbits[k]) - 0.5f;
       r = rintf(sc - noise);
     }
-    bad |= !(fabsf(r) < 8192.0f);
     const float deq = (MODE == FC_DITHERED) ? (r + noise) * cq.step : r * cq.step;
     const float dd = xv - deq;
     // zero padding past P quantises to 0; only dithering's noise would count
@@ -652,10 +691,13 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
   ChunkCode r;
   r.acc = 0;
   r.len = 0;
+  // max |r| of the chunk: two v_max3_f32 with |.| source modifiers.  A NaN may
+  // drop out of the max, but a NaN or infinite r always makes the distortion
+  // non-finite, which k_encode checks per tile before trusting the fast path.
+  const float mabs = vmax3_abs(q[0], q[1], vmax3_abs(q[2], q[3], 0.0f));
+  const bool bad = !(mabs < 8192.0f);
   // small values across the wave (|q| <= 31, the common case): one table read per element
-  bool big = false;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) big |= !(fabsf(q[k]) <= 31.0f);
+  const bool big = !(mabs <= 31.0f);
   if (__ballot(big) == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -827,6 +869,15 @@ __device__ __forceinline__ void emit64(uint32_t* win, uint64_t acc, uint32_t len
   atomicOr(&win[i0], hi >> o);
   atomicOr(&win[i0 + 1], __builtin_amdgcn_alignbit(hi, lo, o));
   atomicOr(&win[i0 + 2], __builtin_amdgcn_alignbit(lo, 0u, o));
+}
+
+// Same for a code of len <= 32 bits: two ds_or_b32.
+__device__ __forceinline__ void emit32(uint32_t* win, uint32_t v, uint32_t len, uint32_t wp) {
+  const uint32_t X = (uint32_t)((uint64_t)v << ((32u - len) & 63u));  // MSB-aligned (len 0: v is 0)
+  const uint32_t o = wp & 31u;
+  const uint32_t i0 = min(wp >> 5, (uint32_t)kWinWords);
+  atomicOr(&win[i0], X >> o);
+  atomicOr(&win[i0 + 1], __builtin_amdgcn_alignbit(X, 0u, o));
 }
 
 // 32 window bits starting at window bit s (any s; reads words s>>5, +1).
@@ -1004,6 +1055,47 @@ __device__ __forceinline__ void slow_emit(const EncodeArgs& a, const ClientQ& cq
   }
 }
 
+// s_waitcnt immediates (gfx9 encoding): vmcnt(0) alone / lgkmcnt(0) alone.
+constexpr int kWaitVm0 = 0x0F70;
+constexpr int kWaitLgkm0 = 0xC07F;
+
+// Tile staging through LDS-DMA (global_load_lds_dwordx4).  DMA instruction b
+// (b = 0..3) fetches the tile's 1-KiB global block b -- coalesced -- into staging
+// words [256 b, +256), permuted inside the block so that lane l's chunk j
+// (tile elements [16 l + 4 j, +4)) lands at word 256 (l >> 4) + 64 j + 4 ((l + 4 j) & 15):
+// the four ds_read_b128 that hand each lane its 16 consecutive elements are then
+// bank-conflict-free (every 16-lane group of a ds_read_b128 covers all 64 banks).
+// Only full tiles of 16-B-aligned rows are staged; returns whether it issued.
+__device__ __forceinline__ bool stage_tile(const EncodeArgs& a, ConstParamPtr cparams, uint32_t ticket,
+                                           uint32_t* stg, int lane) {
+  const int32_t t = (int32_t)div_clients(a, ticket);
+  const int32_t c = (int32_t)(ticket - (uint32_t)t * (uint32_t)a.nclients);
+  const int64_t tile_base = (int64_t)t * kTE;
+  const uint32_t* x = cparams[c].x;
+  if (tile_base + kTE > a.P || ((uintptr_t)x & 15u) || (FC_ABL & 64)) return false;
+  const uint32_t j = (uint32_t)lane >> 4, q = (uint32_t)lane & 15u;
+  const uint32_t* src = x + tile_base + 16u * ((q - 4u * j) & 15u) + 4u * j;
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    __builtin_amdgcn_global_load_lds((const void*)(src + 256 * b), (void*)(stg + 256 * b), 16, 0, 0);
+  return true;
+}
+__device__ __forceinline__ int stage_pos(int lane, int j) {
+  return 256 * (lane >> 4) + 64 * j + 4 * ((lane + 4 * j) & 15);
+}
+// The staging reads are inline asm (their completion is waited for explicitly):
+// the compiler's wait-count pass treats any ds_read of a buffer an LDS-DMA
+// wrote as waiting on that DMA, and would otherwise drain vmcnt -- including
+// the next tile's DMA and the pending tile's stores -- at every tile start.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 stage_read(const uint32_t* stg, int lane, int j) {
+  typedef const __attribute__((address_space(3))) uint32_t* lds_cptr;
+  const lds_cptr p = (lds_cptr)(stg + stage_pos(lane, j));
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(p) : "memory");
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // One wavefront = one workgroup = one 1024-element tile at a time: no barriers,
 // every cross-lane step is DPP / ballot / readlane, the bit window is the
 // wave's own LDS.  Software-pipelined over the wave's tiles: tile n is
@@ -1015,6 +1107,7 @@ template <int MODE, bool INT_IN, bool RCP, bool PRE>
 __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs a) {
   __shared__ uint32_t wins[2][kWinWords + 3];  // double-buffered; + guard words
   __shared__ uint32_t clut[kCodeLut];
+  __shared__ __attribute__((aligned(16))) uint32_t stg[kTE];  // LDS-DMA staging of the next tile
   const int lane = threadIdx.x;
   for (int i = lane; i < kCodeLut; i += kEncThreads) clut[i] = code_lut_entry((uint32_t)i);
   const uint32_t total_tiles = (uint32_t)a.nclients * (uint32_t)a.T;
@@ -1028,11 +1121,17 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
   for (int i = lane; i < 2 * (kWinWords + 3); i += kEncThreads) (&wins[0][0])[i] = 0;
   const uint32_t shard = blockIdx.x % a.nshards;
   uint32_t* my_counter = a.counter + kShardStride * shard;
+  // Tickets run two ahead: the tile after the current one is known when the
+  // current one starts, so its values are staged into LDS (LDS-DMA) while the
+  // current tile computes.
   uint32_t tk = 0;
-  if (FC_ABL & 512) tk = blockIdx.x / a.nshards;
-  else if (lane == 0) tk = atomicAdd(my_counter, 1u);
+  if (lane == 0) tk = atomicAdd(my_counter, 1u);
   uint32_t ticket = shard + a.nshards * uniform(tk);
-  const uint32_t tk_step = (gridDim.x + a.nshards - 1 - shard) / a.nshards;  // blocks on this shard
+  uint32_t tk1 = 0;
+  if (ticket < total_tiles && lane == 0) tk1 = atomicAdd(my_counter, 1u);
+  uint32_t ticket1 = ticket < total_tiles ? shard + a.nshards * uniform(tk1) : ticket;
+  bool staged = ticket < total_tiles && stage_tile(a, cparams, ticket, stg, lane);
+  __builtin_amdgcn_s_waitcnt(kWaitVm0);
   // the pending tile (coded, aggregate published, words not yet stored)
   bool pv = false;
   int32_t pt = 0, pc = 0, pfirst = 0, plast = -1;
@@ -1044,8 +1143,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
     if (!have && !pv) break;
     STAMP(0);
     uint32_t ntk = 0;
-    if (FC_ABL & 512) ntk = tk + tk_step;
-    else if (have && lane == 0) ntk = atomicAdd(my_counter, 1u);  // next ticket
+    if (ticket1 < total_tiles && lane == 0) ntk = atomicAdd(my_counter, 1u);  // ticket after next
     // the pending tile's look-back window (lane i: tile pt-64+i), fetched now and
     // used after this tile's work
     uint64_t pw1 = kFlagPre, pw2 = kFlagPre;
@@ -1058,7 +1156,6 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
     bool nv = false;
     int32_t nt_ = 0, nc = 0, nfirst = 0, nlast = -1;
     uint32_t nbody = 0, ntail = 0;
-    uint32_t next = ticket;
     if (have) {
       uint32_t* win = wins[buf];
       // tickets interleave clients (tile-major) so each client has few tiles in flight
@@ -1067,48 +1164,69 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
       const int64_t tile_base = (int64_t)t * kTE;
       const bool full = tile_base + kTE <= P;
       const ClientParam cp = ld_param(cparams + c);
-      // raw values: chunk j of this lane = tile elements [256 j + 4 lane, +4)
+      // raw values: lane l owns the 16 consecutive tile elements [16 l, 16 l + 16),
+      // chunk j = [16 l + 4 j, +4), from the LDS staging (full, 16-B aligned
+      // tiles) or loaded directly (a client's last, partial tile)
+      const int32_t lrel = 16 * lane;
       uint32_t raw[kChunks][4];
+      if (FC_ABL & 64) {  // diagnostics: synthetic values, no loads
 #pragma unroll
-      for (int j = 0; j < kChunks; ++j) {
-        const int64_t e0 = tile_base + 256 * j + 4 * lane;
-        if (FC_ABL & 64) {
-          raw[j][0] = (uint32_t)e0 * 2654435761u; raw[j][1] = raw[j][0] ^ 0x9E3779B9u;
-          raw[j][2] = raw[j][0] + 12345u; raw[j][3] = raw[j][1] * 3u;
-        } else if (full) {
-          const uint4 v = *(const uint4*)(cp.x + e0);
-          raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) raw[j][k] = (e0 + k < P) ? cp.x[e0 + k] : 0u;
+        for (int j = 0; j < kChunks; ++j) {
+          const uint32_t h = (uint32_t)(tile_base + lrel + 4 * j) * 2654435761u;
+          raw[j][0] = __float_as_uint(((float)((h >> 28) & 15u) - 7.5f) * 0.3f);
+          raw[j][1] = __float_as_uint(((float)((h >> 24) & 15u) - 7.5f) * 0.3f);
+          raw[j][2] = __float_as_uint(((float)((h >> 20) & 15u) - 7.5f) * 0.3f);
+          raw[j][3] = __float_as_uint(((float)((h >> 16) & 15u) - 7.5f) * 0.3f);
         }
+      } else {
+        if (!staged) {  // a client's last (partial) tile or an unaligned row: load into the staging
+#pragma unroll
+          for (int j = 0; j < kChunks; ++j) {
+            const int64_t e0 = tile_base + lrel + 4 * j;
+            uint4 v;
+            if (full) {
+              v = *(const uint4*)(cp.x + e0);
+            } else {
+              v.x = e0 < P ? cp.x[e0] : 0u;
+              v.y = e0 + 1 < P ? cp.x[e0 + 1] : 0u;
+              v.z = e0 + 2 < P ? cp.x[e0 + 2] : 0u;
+              v.w = e0 + 3 < P ? cp.x[e0 + 3] : 0u;
+            }
+            *(uint4*)(stg + stage_pos(lane, j)) = v;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kChunks; ++j) {
+          const uint4 v = stage_read(stg, lane, j);
+          raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
-      // ---- A-D, streamed one chunk (4 elements per lane) at a time: quantise
-      //      + chunk-local code, last nonzero before the chunk (max-scan over
-      //      (chunk, lane) order), prepend its first run code, body-relative
-      //      offset (sum-scan), emit into the window.  Registers stay per-chunk.
+      // the staging is free once read: stage the next tile (waited for after part C)
+      staged = ticket1 < total_tiles && stage_tile(a, cparams, ticket1, stg, lane);
+      // ---- A: quantise + code the lane's four chunks in order.  A chunk's first
+      //      run code comes from the lane's previous nonzero when there is one;
+      //      the lane's very first run code depends on earlier lanes and is
+      //      resolved after the scan.
       float dist = 0.0f;
       int32_t nnz = 0;  // INT_IN: per lane; float input: wave total
-      int32_t carry = -1, wfirst = 0x7FFFFFFF, sfirst = -1;
-      uint64_t lngmask = 0;
-      uint32_t body = 0;
+      int32_t lfirst = -1, llast = -1;  // the lane's first / last nonzero (tile-relative)
+      uint32_t lng = 0, llen = 0;
+      uint64_t cacc[kChunks];
+      uint32_t clen[kChunks];
       {
         const ClientQ cq = client_q_of(cp, pre);
   #pragma unroll
         for (int j = 0; j < kChunks; ++j) {
-          const int32_t rel0 = 256 * j + 4 * lane;
+          const int32_t rel0 = lrel + 4 * j;
           ChunkCode cc;
-          if (INT_IN || (FC_ABL & 8)) {
+          if (INT_IN) {
             int32_t q4[4];
   #pragma unroll
-            for (int k = 0; k < 4; ++k) q4[k] = (FC_ABL & 8) ? (int32_t)(raw[j][k] >> 29) - 3 : (int32_t)raw[j][k];
+            for (int k = 0; k < 4; ++k) q4[k] = (int32_t)raw[j][k];
   #pragma unroll
             for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
-            if (FC_ABL & 2048) {
-              cc.acc = q4[0]; cc.len = q4[1] & 15; cc.lng = 0; cc.first = rel0; cc.last = rel0 + 3;
-            } else {
-              cc = chunk_local(q4, rel0);
-            }
+            cc = chunk_local(q4, rel0);
           } else {
             const uint32_t g = (uint32_t)((tile_base + rel0) >> 2);
             if (MODE == FC_DITHERED && !full)
@@ -1117,56 +1235,60 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
             else
               cc = quant_code_fast<MODE, RCP, PRE>(cq, g, raw[j], rel0, dist, nnz, clut);
           }
-          if (INT_IN || (FC_ABL & 8)) {
-            wfirst = min(wfirst, cc.first >= 0 ? cc.first : 0x7FFFFFFF);
-          } else if (sfirst < 0) {  // the tile's first nonzero: first chunk with one, lowest lane
-            const uint64_t fm = __ballot(cc.first >= 0);
-            if (fm) sfirst = __builtin_amdgcn_readlane(cc.first, (int)__builtin_ctzll(fm));
-          }
-          int32_t prev;
-          uint32_t off;
-          if (FC_ABL & 128) {
-            prev = cc.last - 4;
-            carry = max(carry, cc.last);
-            chunk_prepend(cc, prev);
-            lngmask |= __ballot(cc.lng != 0);
-            off = 16 * lane + 1024 * j;
-            body += 1024;
-          } else {
-            const int32_t im = dpp_incl_max(cc.last);
-            prev = max(dpp_shr1(im, -1), carry);
-            carry = max(carry, lane63(im));
-            chunk_prepend(cc, prev);
-            lngmask |= __ballot(cc.lng != 0);
-            const uint32_t is = dpp_incl_sum(cc.len);
-            off = body + is - cc.len;
-            body += (uint32_t)lane63((int32_t)is);
-          }
-          // codes past the window land in the guard words (the tile is then slow)
-          if (FC_ABL & 1) asm volatile("" :: "v"((uint32_t)cc.acc), "v"(off));
-          else emit64(win, cc.acc, cc.len, kPre + off);
+          chunk_prepend(cc, llast);  // no-op without an earlier nonzero in the lane
+          lfirst = lfirst < 0 ? cc.first : lfirst;
+          llast = cc.last >= 0 ? cc.last : llast;
+          lng |= cc.lng;
+          cacc[j] = cc.acc;
+          clen[j] = cc.len;
+          llen += cc.len;
           FC_CHUNK_BARRIER;
         }
       }
+      // ---- B: one scan pair per tile -- last nonzero before each lane (max-scan)
+      //      gives the lane's first run code, then code offsets (sum-scan)
+      const int32_t im = dpp_incl_max(llast);
+      const int32_t lprev = dpp_shr1(im, -1);  // -1: no nonzero in earlier lanes of this tile
+      const int32_t tile_last = lane63(im);
+      const bool lrun = lfirst >= 0 && lprev >= 0;
+      const uint32_t dv = lrun ? (uint32_t)(lfirst - lprev) : 0u;
+      const uint32_t R = lrun ? glen(dv) : 0u;
+      const uint32_t ltot = R + llen;
+      const uint32_t is = dpp_incl_sum(ltot);
+      const uint32_t body = (uint32_t)lane63((int32_t)is);
+      const uint64_t lngmask = __ballot(lng != 0);
+      // ---- C: emit the lane's run code and chunks (codes past the window land in
+      //      the guard words; the tile is then slow)
+      {
+        uint32_t o = kPre + is - ltot;
+        emit32(win, dv, R, o);
+        o += R;
+  #pragma unroll
+        for (int j = 0; j < kChunks; ++j) {
+          emit64(win, cacc[j], clen[j], o);
+          o += clen[j];
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(kWaitVm0);  // next tile staged (and the look-back window loaded)
       STAMP(1);
-      // fast path: no long chunk, and prefix + body + trailing code + one funnel
-      // word fit the wave's window
-      const bool fast = lngmask == 0 && kPre + body + 96u <= 32u * kWinWords;
+      // fast path: no long chunk, prefix + body + trailing code + one funnel word
+      // fit the wave's window, and a finite distortion (no NaN / infinite r)
+      const float dsum = INT_IN ? 0.0f : wave_sum_f(dist);
+      const bool fast = lngmask == 0 && kPre + body + 96u <= 32u * kWinWords &&
+                        (INT_IN || dsum <= 3.4028235e38f);
       STAMP(2);
 
       const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;
-      const int32_t tile_last = carry;
-      const int32_t tile_first = (INT_IN || (FC_ABL & 8)) ? wave_min_i(wfirst) : sfirst;
+      const uint64_t fm = __ballot(lfirst >= 0);  // lanes are in element order
+      const int32_t tile_first = fm ? __builtin_amdgcn_readlane(lfirst, (int)__builtin_ctzll(fm)) : -1;
       if (fast && !(FC_ABL & 32)) {
-        const float d = wave_sum_f(dist);
-        const int32_t n = (INT_IN || (FC_ABL & 8)) ? wave_sum_i(nnz) : nnz;
+        const float d = dsum;
+        const int32_t n = INT_IN ? wave_sum_i(nnz) : nnz;
         if (lane == 0) {
           if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
           if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t] = n;
         }
       }
-      next = shard + a.nshards * uniform(ntk);
-      if (FC_ABL & 512) tk = ntk;
       STAMP(3);
       uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t);
       if (!fast) {
@@ -1298,7 +1420,10 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
     pbody = nbody;
     ptail = ntail;
     buf ^= 1;
-    ticket = have ? next : ticket;
+    if (have) {
+      ticket = ticket1;
+      if (ticket1 < total_tiles) ticket1 = shard + a.nshards * uniform(ntk);
+    }
   }
 #ifdef FC_STAMPS
   if (lane == 0)
