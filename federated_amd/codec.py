@@ -183,6 +183,26 @@ def decode_accumulate(batch, sum_in=None, want_sum=True, out=None, step=1.0, noi
   return (sum_out if want_sum else None), out, err
 
 
+def decode_accumulate_scaled(batch, client_scale, out=None, fsum_in=None, stream=None, err=None):
+  """QSGD server sum: out = [fsum_in +] sum_c float(q_c) * client_scale[c] (float32).
+
+  Returns (out, err tensor).
+  """
+  _lib.require_gpu()
+  device = batch.device
+  if out is None:
+    out = torch.empty(batch.P, dtype=torch.float32, device=device)
+  if err is None:
+    err = torch.zeros(1, dtype=torch.int32, device=device)
+  client_scale = torch.as_tensor(client_scale, dtype=torch.float32).to(device).contiguous()
+  assert client_scale.numel() == batch.nclients
+  _lib.call("fc_decode_accumulate_scaled", _lib.ptr(batch.stream), _lib.ptr(batch.stream_off),
+            _lib.ptr(batch.stream_cap), _lib.ptr(batch.idx), batch.nclients, batch.P,
+            _lib.ptr(client_scale), _lib.ptr(fsum_in), _lib.ptr(out), _lib.ptr(err),
+            _lib.stream_handle(stream))
+  return out, err
+
+
 def finalize(batch, stream=None):
   """Per-client float64 sum of squared error and int64 nonzero count (device)."""
   dist = torch.empty(batch.nclients, dtype=torch.float64, device=batch.device)

@@ -1563,6 +1563,8 @@ struct DecodeArgs {
   float step;
   const float* noise_sum;
   int32_t* err;
+  const float* client_scale;  // FACC: per-client dequantisation step
+  const float* fsum_in;       // FACC: optional float partial sum to add
 };
 
 // MSB-first bit reader over one client's code: a 64-bit window plus one
@@ -1839,8 +1841,17 @@ __device__ __forceinline__ uint32_t lut_entry(uint32_t x) {
 // by slow_code (the reader then restarts after it).
 // One table step: up to two codes from the next 12 window bits (caller checked
 // e & 15 != 0, i.e. the first code fits).  Returns the bits consumed.
+// Accumulator add: int32 client sum, or (QSGD) the float32 sum of each client's
+// dequantised value f32(v) * scale.
+template <bool FACC>
+__device__ __forceinline__ void acc_add(int32_t* my, uint32_t i, int32_t v, float scale) {
+  if (FACC) atomicAdd((float*)my + i, (float)v * scale);
+  else atomicAdd(my + i, v);
+}
+
+template <bool FACC>
 __device__ __forceinline__ uint32_t table_step(uint32_t e, int32_t rem, int32_t& rel, int32_t* my,
-                                               uint32_t& bad) {
+                                               uint32_t& bad, float scale) {
   const uint32_t L1 = e & 15u, L2 = (e >> 4) & 15u;
   const bool two = (e >> 30) == 2u && (int32_t)L2 <= rem;  // a second code past the segment is not ours
   const int32_t rel1 = rel + (int32_t)((e >> 8) & 31u);
@@ -1849,8 +1860,8 @@ __device__ __forceinline__ uint32_t table_step(uint32_t e, int32_t rem, int32_t&
   const int32_t v2 = two ? (int32_t)((e >> 24) & 63u) - 32 : 0;
   rel = two ? rel2 : rel1;
   bad |= (uint32_t)rel >= (uint32_t)kTE;
-  atomicAdd(&my[min((uint32_t)rel1, (uint32_t)kTE - 1)], v1);
-  atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v2);
+  acc_add<FACC>(my, min((uint32_t)rel1, (uint32_t)kTE - 1), v1, scale);
+  if (!FACC || v2 != 0) acc_add<FACC>(my, min((uint32_t)rel, (uint32_t)kTE - 1), v2, scale);
   return two ? L2 : L1;
 }
 
@@ -1860,9 +1871,10 @@ __device__ __forceinline__ uint32_t table_step(uint32_t e, int32_t rem, int32_t&
 // two short codes) or decodes a longer code arithmetically from the top 32 bits
 // (longer than 32 bits: slow_code, then the reader restarts); step B is a
 // table step when >= 12 bits remain in the window.  Segments are < 2^31 bits.
+template <bool FACC>
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
                                                uint64_t b1, int32_t rel, int32_t* my,
-                                               const uint32_t* lut, int32_t* err) {
+                                               const uint32_t* lut, int32_t* err, float scale) {
   SegReader r;
   r.init(base, cap, b0);
   int32_t rem = (int32_t)(b1 - b0);
@@ -1871,7 +1883,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
     uint32_t L;
     if (e & 15u) {
-      L = table_step(e, rem, rel, my, bad);
+      L = table_step<FACC>(e, rem, rel, my, bad, scale);
       r.win <<= L;
       r.nwin -= (int32_t)L;
     } else {
@@ -1901,14 +1913,14 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       }
       rel += (int32_t)d;
       bad |= (uint32_t)rel >= (uint32_t)kTE;
-      atomicAdd(&my[min((uint32_t)rel, (uint32_t)kTE - 1)], v);
+      acc_add<FACC>(my, min((uint32_t)rel, (uint32_t)kTE - 1), v, scale);
     }
     rem -= (int32_t)L;
 #pragma unroll
     for (int st = 1; st < FC_DEC_STEPS; ++st) {
       e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
       if (rem > 0 && r.nwin >= kLutBits && (e & 15u)) {
-        L = table_step(e, rem, rel, my, bad);
+        L = table_step<FACC>(e, rem, rel, my, bad, scale);
         r.win <<= L;
         r.nwin -= (int32_t)L;
         rem -= (int32_t)L;
@@ -1925,6 +1937,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 // Persistent: each workgroup builds the decode table once, then walks tiles
 // (tiles_per_wg at a time) with one lane per client segment, accumulating the
 // clients' values in LDS and writing the tile's sum / dequantised values.
+template <bool FACC>
 __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
   extern __shared__ int32_t smem[];  // [kLutSize] table, then [tiles_per_wg][kTE] sums
   uint32_t* lut = (uint32_t*)smem;
@@ -1949,13 +1962,20 @@ __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
         const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
         if (bend <= bstart) continue;
         const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
-        decode_segment(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart, bend, rel, my, lut, a.err);
+        decode_segment<FACC>(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart, bend, rel, my, lut, a.err,
+                              FACC ? a.client_scale[c] : 0.0f);
       }
     }
     __syncthreads();
     for (int i = tid; i < tiles_per_wg * kTE; i += kThreads) {
       const int64_t e = t0 * kTE + i;
       if (e >= a.P) break;
+      if (FACC) {  // float32 sum of dequantised clients (+ a float partial sum)
+        float f = __int_as_float(acc[i]);
+        if (a.fsum_in) f = a.fsum_in[e] + f;
+        a.out[e] = f;
+        continue;
+      }
       int32_t v = acc[i];
       if (a.sum_in) v = (int32_t)((uint32_t)v + (uint32_t)a.sum_in[e]);
       if (a.sum_out) a.sum_out[e] = v;
@@ -2285,6 +2305,43 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   return check_launch("k_encode_exact");
 }
 
+// Shared launcher of k_decode (int32 client sum, or float sum of scaled clients).
+int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap,
+                  const uint64_t* idx, int32_t nclients, int64_t P, int32_t* err, void* stream) {
+  if (nclients <= 0) return fail(-1, "nclients must be > 0");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
+  if (!stream_buf || !stream_off || !stream_cap || !idx || !err) return fail(-1, "null required pointer");
+  a.stream_buf = stream_buf;
+  a.stream_off = stream_off;
+  a.stream_cap = stream_cap;
+  a.idx = idx;
+  a.nclients = nclients;
+  a.P = P;
+  a.T = (int32_t)tiles_for(P);
+  a.err = err;
+  int lpt = 256;
+  while (lpt > 64 && lpt / 2 >= nclients) lpt /= 2;
+  a.lanes_per_tile = lpt;
+  const bool facc = a.client_scale != nullptr;
+  void (*kern)(DecodeArgs) = facc ? k_decode<true> : k_decode<false>;
+  const int tpw = kThreads / lpt;
+  const size_t lds = (size_t)kLutSize * 4 + (size_t)tpw * kTE * sizeof(int32_t);
+  int dev = 0, ncu = 256, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  const int64_t ngroups = (a.T + tpw - 1) / tpw;
+  // 5 workgroups/CU: more waves only add L2 line thrash (measured 4.2 ms at 5/CU vs 5.0 at 7/CU)
+  int64_t max_grid = (int64_t)ncu * std::min(per_cu, 5);
+  if (const char* g = getenv("FEDCODEC_DEC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
+  const dim3 grid((unsigned)std::min<int64_t>(ngroups, max_grid));
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(err, 0, sizeof(int32_t), s) != hipSuccess) return fail(-10, "memset err");
+  hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, s, a);
+  return check_launch("k_decode");
+}
+
 }  // namespace
 
 extern "C" {
@@ -2346,43 +2403,26 @@ int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off, c
                          const uint64_t* idx, int32_t nclients, int64_t P, const int32_t* sum_in,
                          int32_t* sum_out, float* out, float step, const float* noise_sum, int32_t* err,
                          void* stream) {
-  if (nclients <= 0) return fail(-1, "nclients must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
-  if (!stream_buf || !stream_off || !stream_cap || !idx || !err) return fail(-1, "null required pointer");
   if (!sum_out && !out) return fail(-1, "one of sum_out / out required");
-  DecodeArgs a;
-  a.stream_buf = stream_buf;
-  a.stream_off = stream_off;
-  a.stream_cap = stream_cap;
-  a.idx = idx;
-  a.nclients = nclients;
-  a.P = P;
-  a.T = (int32_t)tiles_for(P);
-  int lpt = 256;
-  while (lpt > 64 && lpt / 2 >= nclients) lpt /= 2;
-  a.lanes_per_tile = lpt;
+  DecodeArgs a{};
   a.sum_in = sum_in;
   a.sum_out = sum_out;
   a.out = out;
   a.step = step;
   a.noise_sum = noise_sum;
-  a.err = err;
-  const int tpw = kThreads / lpt;
-  const size_t lds = (size_t)kLutSize * 4 + (size_t)tpw * kTE * sizeof(int32_t);
-  int dev = 0, ncu = 256, per_cu = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode, kThreads, lds) != hipSuccess || per_cu < 1)
-    per_cu = 1;
-  const int64_t ngroups = (a.T + tpw - 1) / tpw;
-  // 5 workgroups/CU: more waves only add L2 line thrash (measured 4.2 ms at 5/CU vs 5.0 at 7/CU)
-  int64_t max_grid = (int64_t)ncu * std::min(per_cu, 5);
-  if (const char* g = getenv("FEDCODEC_DEC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
-  const dim3 grid((unsigned)std::min<int64_t>(ngroups, max_grid));
-  hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(err, 0, sizeof(int32_t), s) != hipSuccess) return fail(-10, "memset err");
-  hipLaunchKernelGGL(k_decode, grid, dim3(kThreads), lds, s, a);
-  return check_launch("k_decode");
+  return decode_common(a, stream_buf, stream_off, stream_cap, idx, nclients, P, err, stream);
+}
+
+int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream_off,
+                                const int64_t* stream_cap, const uint64_t* idx, int32_t nclients, int64_t P,
+                                const float* client_scale, const float* fsum_in, float* out, int32_t* err,
+                                void* stream) {
+  if (!out || !client_scale) return fail(-1, "null required pointer");
+  DecodeArgs a{};
+  a.out = out;
+  a.client_scale = client_scale;
+  a.fsum_in = fsum_in;
+  return decode_common(a, stream_buf, stream_off, stream_cap, idx, nclients, P, err, stream);
 }
 
 int fc_dequantize(const int32_t* sum, int64_t P, float step, const float* noise_sum, float* out,

@@ -23,6 +23,9 @@
  *                          accumulate/merge (elias_gamma_encode.py:63-88) =
  *                          tfc.run_length_gamma_decode + int32 sum, optionally fused
  *                          with the server dequantize (quantize_encode.py:189-190)
+ *   fc_decode_accumulate_scaled  QSGDFactory sum_encoded_value accumulate
+ *                          (comparison_methods/qsgd.py:85-112): decode + per-client
+ *                          dequantize(norm / num_steps) + float32 sum
  *   fc_noise_sum           federated_sum(noise) for dithered mode (quantize_encode.py:183)
  *   fc_client_norms        normalize_fn: mean_magnitude / max_magnitude /
  *                          dimensionless_norm (quantize_utils.py:20-29,
@@ -118,6 +121,14 @@ int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off,
                          const int64_t* stream_cap, const uint64_t* idx, int32_t nclients,
                          int64_t P, const int32_t* sum_in, int32_t* sum_out, float* out,
                          float step, const float* noise_sum, int32_t* err, void* stream);
+
+/* QSGD server side: out[i] = [fsum_in[i] +] sum over clients of
+ * float(q_c[i]) * client_scale[c] in float32 (summation order unspecified: the
+ * reference's client-order float sum is matched within a tolerance). */
+int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream_off,
+                                const int64_t* stream_cap, const uint64_t* idx, int32_t nclients,
+                                int64_t P, const float* client_scale, const float* fsum_in,
+                                float* out, int32_t* err, void* stream);
 
 /* out = (float(sum) [+ noise_sum]) * step (FTZ as TF-CPU). */
 int fc_dequantize(const int32_t* sum, int64_t P, float step, const float* noise_sum,

@@ -7,6 +7,7 @@ the C run-length-gamma restatement, for a list of client values:
 * ``elias_gamma_sum_next``   aggregators/elias_gamma_encode.py:63-114
 * ``stochastic_quantize_next`` aggregators/stochastic_quantize.py:57-88 (SumFactory inner)
 * ``one_bit_sgd_next``       aggregators/comparison_methods/one_bit_sgd.py:45-112
+* ``qsgd_next``              aggregators/comparison_methods/qsgd.py:62-146
 
 Float reductions (distortion, 1-bit means, one-bit decoded sums) follow TF's
 float32 semantics up to summation order; tests compare them with tolerances.
@@ -106,3 +107,37 @@ def one_bit_sgd_next(client_values, threshold=0.0):
     acc = (acc + dec).astype(np.float32)                                     # :97-100
   return acc, collections.OrderedDict(avg_bitrate=F32((F32(P) + F32(64.0)) / F32(P)),
                                       avg_distortion=F32(np.mean(dists)))
+
+
+def l2_norm(x):
+  """tf.norm(value, ord=2) (qsgd.py:66): TF reduces in float32 in an unspecified
+  order; restated as the correctly rounded float32 of a float64 sum (the HIP
+  path's fc_client_norms does the same), so q can be compared bit-exactly."""
+  x = qu.ftz(np.asarray(x, np.float32)).astype(np.float64)
+  return F32(np.sqrt(np.sum(x * x)))
+
+
+def qsgd_next(client_values, num_steps, seeds):
+  """QSGDFactory round: (float32 result, measurements, codes)."""
+  xs = [np.asarray(v, np.float32).reshape(-1) for v in client_values]
+  P = xs[0].size
+  acc = np.zeros(P, np.float32)                                              # :88-89
+  dists, sps, lengths, codes = [], [], [], []
+  for c, x in enumerate(xs):
+    norm = l2_norm(x)                                                         # :66
+    with np.errstate(divide="ignore", invalid="ignore"):
+      step = F32(norm / F32(num_steps))                                       # :67
+    q = qu.stochastic_quantize(x, step, tuple(seeds[c]))                      # :68-69
+    deq = qu.uniform_dequantize(q, step)                                      # :70-71
+    d = qu.ftz(x) - deq
+    dists.append(F32(np.sum(d.astype(np.float64) ** 2) / P))                 # :72-74
+    sps.append(F32((F32(P) - F32(np.count_nonzero(q))) / F32(P)))            # :75-77
+    code, _ = codec.run_length_gamma_encode(q)                                # :78
+    codes.append(code)
+    lengths.append(np.float64(32.0 + 8.0 * len(code)))                        # :27-32
+    acc = (acc + deq).astype(np.float32)                                      # :92-97 (client order)
+  measurements = collections.OrderedDict(
+      avg_bitrate=np.float64(np.mean(lengths) / np.float64(P)),              # :127-134
+      avg_distortion=F32(np.mean(dists)),
+      avg_sparsity=F32(np.mean(sps)))
+  return acc, measurements, codes

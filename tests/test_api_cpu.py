@@ -120,3 +120,11 @@ def test_to_type():
   assert t.num_elements == 8 and t.is_tensor()
   s = tc.to_type([(np.float32, (2,)), (np.int32, (3,))])
   assert not s.is_tensor() and not tc.is_structure_of_floats(s)
+
+
+def test_qsgd_create():
+  from federated_amd.aggregators.comparison_methods import qsgd  # pylint: disable=g-import-not-at-top
+  process = qsgd.QSGDFactory(7.0).create((np.float32, (3,)))
+  assert process.initialize() == ()
+  with pytest.raises(ValueError):  # qsgd_test.py:60-66
+    qsgd.QSGDFactory(1.0).create((np.int32, (3,)))

@@ -181,3 +181,51 @@ def test_decoder_rejects_malformed_stream(gpu):
   b.stream.zero_()  # a run of zeros longer than 31 bits is not a gamma code
   _, _, err = codec.decode_accumulate(b)
   assert int(err.item()) != 0
+
+
+# qsgd_test.py:72-142 known answers, through the HIP path
+@pytest.mark.parametrize("values,num_steps,want,bitrate", [
+    ([[1.0]], 1.0, [1.0], 40.0),
+    ([[1.0], [2.0]], 2.0, [3.0], 40.0),
+    ([[2.0, 3.0, 6.0]] * 2, 7.0, [4.0, 6.0, 12.0], 56.0 / 3.0),
+])
+def test_qsgd_reference_execution(gpu, values, num_steps, want, bitrate):
+  from federated_amd.aggregators.comparison_methods import qsgd  # pylint: disable=g-import-not-at-top
+  process = qsgd.QSGDFactory(num_steps).create((np.float32, (len(values[0]),)))
+  out = process.next(process.initialize(), [np.asarray(v, np.float32) for v in values])
+  np.testing.assert_allclose(out.result, want, rtol=1e-6)
+  assert out.measurements["avg_bitrate"] == np.float64(bitrate)
+  assert out.measurements["avg_distortion"] == 0.0 and out.measurements["avg_sparsity"] == 0.0
+
+
+@pytest.mark.parametrize("P,C", [(5, 2), (4099, 3), (300007, 6)])
+def test_qsgd_matches_oracle(gpu, P, C):
+  from federated_amd.aggregators.comparison_methods import qsgd  # pylint: disable=g-import-not-at-top
+  rng = np.random.default_rng(P + C)
+  xs = [(rng.standard_normal(P) * rng.uniform(0.01, 3)).astype(np.float32) for _ in range(C)]
+  seeds = np.array([[40 + c, 7 * c] for c in range(C)], np.int64)
+  process = qsgd.QSGDFactory(127.0).create((np.float32, (P,)))
+  out = process.next(process.initialize(), xs, seeds=seeds)
+  want, m, codes = oagg.qsgd_next(xs, 127.0, seeds=seeds)
+  # q and the codes are exact given the norm; the server sum is a float32 sum over
+  # clients in an unspecified order: |err| <= C ulp-scale of the largest term
+  scale = max(np.max(np.abs(w)) for w in [want]) + 1e-30
+  np.testing.assert_allclose(out.result, want, rtol=1e-6 * C, atol=1e-6 * C * scale)
+  assert out.measurements["avg_bitrate"] == m["avg_bitrate"]
+  assert out.measurements["avg_sparsity"] == m["avg_sparsity"]
+  np.testing.assert_allclose(out.measurements["avg_distortion"], m["avg_distortion"], rtol=1e-5)
+
+
+def test_qsgd_codes_bit_exact(gpu):
+  """The fused encoder with a per-client step reproduces the oracle's bytes."""
+  rng = np.random.default_rng(11)
+  P, C = 70001, 3
+  xs = [(rng.standard_normal(P) * 0.1).astype(np.float32) for _ in range(C)]
+  seeds = np.array([[9, c] for c in range(C)], np.int64)
+  _, _, codes = oagg.qsgd_next(xs, 15.0, seeds=seeds)
+  norms = np.array([oagg.l2_norm(x) for x in xs], np.float32)
+  steps = torch.from_numpy((norms / np.float32(15.0)).astype(np.float32)).to(gpu)
+  batch = codec.quantize_encode_checked([torch.from_numpy(x).to(gpu) for x in xs], 1.0,
+                                        torch.from_numpy(seeds), _lib.STOCHASTIC, norms=steps)
+  for c in range(C):
+    assert batch.client_code(c) == codes[c]

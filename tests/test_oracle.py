@@ -202,3 +202,27 @@ def test_golden_fixtures_reproduce():
     code, nbits = ocodec.run_length_gamma_encode(g["rl_in_" + name])
     assert nbits == int(g["rl_bits_" + name])
     assert code == g["rl_code_" + name].tobytes()
+
+
+# qsgd_test.py:72-141 (known answers of the QSGD round)
+@pytest.mark.parametrize("values,num_steps,want,bitrate", [
+    ([[1.0]], 1.0, [1.0], 40.0),                                     # :72-94
+    ([[1.0], [2.0]], 2.0, [3.0], 40.0),                              # :96-118
+    ([[2.0, 3.0, 6.0]] * 2, 7.0, [4.0, 6.0, 12.0], 56.0 / 3.0),      # :120-142
+])
+def test_qsgd_known_answers(values, num_steps, want, bitrate):
+  res, m, _ = oagg.qsgd_next(values, num_steps, seeds=[(1, 2), (3, 4)])
+  np.testing.assert_allclose(res, want, rtol=1e-6)
+  assert m["avg_bitrate"] == np.float64(bitrate)
+  assert m["avg_distortion"] == 0.0 and m["avg_sparsity"] == 0.0
+
+
+def test_qsgd_different_clients_bounds():
+  # qsgd_test.py:144-172: result within the stochastic-rounding bounds
+  res, m, _ = oagg.qsgd_next([[2.0, 3.0, 6.0], [1.0, 1.0, 1.0]], 7.0, seeds=[(5, 6), (7, 8)])
+  lo = np.sqrt(3.0) / 7.0 * 4.0
+  hi = np.sqrt(3.0) / 7.0 * 5.0
+  assert np.all(res - np.array([2.0 + lo, 3.0 + lo, 6.0 + lo]) >= -1e-6)
+  assert np.all(res - np.array([2.0 + hi, 4.0 + hi, 6.0 + hi]) <= 1e-6)
+  assert m["avg_bitrate"] == np.float64(56.0 / 3.0)
+  assert m["avg_distortion"] <= max(1.0 - lo, hi - 1.0) ** 2 / 2.0
