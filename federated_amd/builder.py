@@ -32,9 +32,11 @@ import numpy as np
 import torch
 
 from federated_amd import _lib
+from federated_amd import builder_configs
 from federated_amd import codec
 from federated_amd import tff_compat as tc
 from federated_amd.aggregators import quantize_encode
+from federated_amd.aggregators import quantize_encode_client_lambda
 
 F32 = np.float32
 
@@ -197,6 +199,35 @@ def build_quantization_encode_aggregator(
                                                   step_size_sched,
                                                   step_size_sched_hparam,
                                                   min_step_size)
+
+  return configure_aggregator(factory, rotation, concatenate, zeroing, clipping,
+                              weighted)
+
+
+def build_vote_step_size_aggregator(
+    step_size: float,
+    rounding_type: str = "uniform",
+    sampling_width: float = 1.15,
+    rotation: str = "identity",
+    concatenate: bool = True,
+    zeroing: bool = True,
+    clipping: bool = True,
+    weighted: bool = True):
+  """Creates an aggregation factory for client voting experiments (builder.py:528-579)."""
+  if step_size not in builder_configs.LAGRANGE_MULTIPLIER_VALUES.keys():
+    raise ValueError(
+        "Expected `step_size` to be one one of [0.05, 0.1, 0.25, 0.5, 1.0, "
+        f"2.0, 2.5, 3.75, 5.0, 7.5, 10.0], found {step_size}.")
+  if rounding_type not in ["uniform", "stochastic", "dithered"]:
+    raise ValueError("Expected `rounding_type` to be one one of [\"uniform\", "
+                     f"\"stochastic\", \"dithered\"], found {rounding_type}.")
+
+  lagrange_multiplier = builder_configs.LAGRANGE_MULTIPLIER_VALUES[step_size]
+  step_size_options = [
+      step_size * scale for scale in sampling_width**np.linspace(-3, 3, 7)
+  ]
+  factory = quantize_encode_client_lambda.QuantizeEncodeClientLambdaFactory(
+      lagrange_multiplier, step_size, step_size_options, rounding_type)
 
   return configure_aggregator(factory, rotation, concatenate, zeroing, clipping,
                               weighted)

@@ -203,6 +203,29 @@ def decode_accumulate_scaled(batch, client_scale, out=None, fsum_in=None, stream
   return out, err
 
 
+def vote_lengths(xs, steps, seeds, mode, stream=None):
+  """Per client and step option: exact code bits and sum (x - deq)^2 (fc_vote_lengths).
+
+  Returns (bits int64 [C, K], dist float64 [C, K]) on the device.
+  """
+  _lib.require_gpu()
+  rows = _rows(xs, torch.float32)
+  P = rows[0].numel()
+  device = rows[0].device
+  C = len(rows)
+  ptrs = _ptr_array(rows, device)
+  steps = torch.as_tensor(np.asarray(steps, np.float32)).to(device)
+  K = steps.numel()
+  seeds = torch.as_tensor(seeds, dtype=torch.int64).reshape(C, 2).to(device)
+  bits = torch.empty(C * K, dtype=torch.int64, device=device)
+  dist = torch.empty(C * K, dtype=torch.float64, device=device)
+  need = int(_lib.load().fc_vote_workspace_bytes(C, P, K))
+  ws = torch.empty(_round_up(need, 256), dtype=torch.uint8, device=device)
+  _lib.call("fc_vote_lengths", _lib.ptr(ptrs), C, P, _lib.ptr(steps), K, _lib.ptr(seeds), int(mode),
+            _lib.ptr(bits), _lib.ptr(dist), _lib.ptr(ws), ws.numel(), _lib.stream_handle(stream))
+  return bits.reshape(C, K), dist.reshape(C, K)
+
+
 def finalize(batch, stream=None):
   """Per-client float64 sum of squared error and int64 nonzero count (device)."""
   dist = torch.empty(batch.nclients, dtype=torch.float64, device=batch.device)

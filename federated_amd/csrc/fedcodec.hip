@@ -2178,6 +2178,160 @@ __global__ void k_onebit_decode_sum(const uint32_t* masks, const float* means, i
   out[i] = s;
 }
 
+
+// ---------------------------------------------------------------------------
+// Step-size vote (quantize_encode_client_lambda.py:105-130): for every client
+// and every step option, the distortion and the exact run-length-gamma code
+// length of its quantisation -- lengths only, nothing is packed.  The TF
+// stateless stream is drawn once per element and shared by all options (the
+// reference re-draws the same stream with the same seed for each option).
+// Pass 1 (k_vote_tiles): one wave per (client, 1024-element tile) computes, per
+// option, the tile's body bits (every code after its first nonzero's run code),
+// first / last nonzero and distortion.  Pass 2 (k_vote_finalize): one
+// workgroup per (client, option) stitches the tiles (run code of each tile's
+// first nonzero from the last nonzero before it, trailing zero run).
+// ---------------------------------------------------------------------------
+struct VoteRec {
+  uint32_t body;
+  int32_t first, last;
+  float dist;
+};
+
+struct VoteArgs {
+  const float* const* xs;
+  int32_t nclients;
+  int64_t P;
+  int32_t T;
+  int32_t K;
+  const float* steps;  // [K]
+  const int64_t* seeds;  // [2 * nclients]
+  VoteRec* rec;          // [nclients][K][T]
+  int64_t* bits;         // [nclients * K]
+  double* dist;          // [nclients * K]
+};
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_vote_tiles(VoteArgs a) {
+  const int lane = threadIdx.x;
+  const int64_t total = (int64_t)a.nclients * a.T;
+  for (int64_t tk = blockIdx.x; tk < total; tk += gridDim.x) {
+    const int32_t c = (int32_t)(tk / a.T);
+    const int32_t t = (int32_t)(tk - (int64_t)c * a.T);
+    const int64_t tile_base = (int64_t)t * kTE;
+    const float* x = a.xs[c];
+    float xv[16];
+    uint32_t rb[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t e = tile_base + 16 * lane + i;
+      xv[i] = e < a.P ? x[e] : 0.0f;
+    }
+    Key4 key{0, 0, 0, 0};
+    if (MODE != FC_UNIFORM) key = tf_seed_scramble(a.seeds[2 * c], a.seeds[2 * c + 1]);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint4 r = make_uint4(0, 0, 0, 0);
+      if (MODE != FC_UNIFORM) r = philox_group(key, (uint32_t)((tile_base + 16 * lane + 4 * g) >> 2));
+      rb[4 * g] = r.x; rb[4 * g + 1] = r.y; rb[4 * g + 2] = r.z; rb[4 * g + 3] = r.w;
+    }
+    for (int k = 0; k < a.K; ++k) {
+      const float step = a.steps[k];
+      float dist = 0.0f;
+      int32_t lfirst = -1, prev = -1;
+      uint32_t len = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int32_t rel = 16 * lane + i;
+        const bool valid = tile_base + rel < a.P;
+        float deq, noise;
+        int32_t q = quantize_one<MODE>(xv[i], step, 0.0f, rb[i], deq, noise);
+        const float dd = xv[i] - deq;
+        dist = valid ? dist + dd * dd : dist;
+        q = valid ? q : 0;
+        if (q != 0) {
+          uint32_t L = 1u + glen(mag_u32(q));
+          if (prev >= 0) L += glen((uint32_t)(rel - prev));
+          else lfirst = rel;
+          len += L;
+          prev = rel;
+        }
+      }
+      const int32_t im = wave_incl_max(prev, lane);
+      const int32_t lprev = __shfl_up(im, 1, 64);
+      const uint32_t R = (lfirst >= 0 && lane > 0 && lprev >= 0) ? glen((uint32_t)(lfirst - lprev)) : 0u;
+      const uint32_t body = (uint32_t)wave_sum_i((int32_t)(len + R));
+      const float d = wave_sum_f(dist);
+      const uint64_t fm = __ballot(lfirst >= 0);
+      const int32_t tfirst = __shfl(lfirst, fm ? (int)__builtin_ctzll(fm) : 0, 64);
+      const int32_t tlast = __shfl(im, 63, 64);
+      if (lane == 0) {
+        VoteRec r;
+        r.body = body;
+        r.first = fm ? tfirst : -1;
+        r.last = tlast;
+        r.dist = d;
+        a.rec[((int64_t)c * a.K + k) * a.T + t] = r;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_vote_finalize(VoteArgs a) {
+  __shared__ int64_t carry[256];
+  __shared__ unsigned long long rbits[256];
+  __shared__ double rdist[256];
+  const int tid = threadIdx.x;
+  const int64_t ck = blockIdx.x;
+  const VoteRec* rec = a.rec + ck * a.T;
+  const int32_t chunk = (a.T + 255) / 256;
+  const int32_t t0 = min(a.T, tid * chunk), t1 = min(a.T, t0 + chunk);
+  int64_t mylast = -1;
+  for (int32_t t = t0; t < t1; ++t)
+    if (rec[t].last >= 0) mylast = (int64_t)t * kTE + rec[t].last;
+  carry[tid] = mylast;
+  __syncthreads();
+  if (tid == 0) {  // exclusive prefix max over threads (tiles are in thread order)
+    int64_t m = -1;
+    for (int i = 0; i < 256; ++i) {
+      const int64_t v = carry[i];
+      carry[i] = m;
+      m = v > m ? v : m;
+    }
+  }
+  __syncthreads();
+  int64_t prevlast = carry[tid];
+  unsigned long long b = 0;
+  double dd = 0.0;
+  for (int32_t t = t0; t < t1; ++t) {
+    const VoteRec r = rec[t];
+    b += r.body;
+    dd += (double)r.dist;
+    if (r.first >= 0) {
+      b += glen((uint32_t)((int64_t)t * kTE + r.first - prevlast));
+      prevlast = (int64_t)t * kTE + r.last;
+    }
+  }
+  rbits[tid] = b;
+  rdist[tid] = dd;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      rbits[tid] += rbits[tid + o];
+      rdist[tid] += rdist[tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    unsigned long long total = rbits[0];
+    int64_t L = -1;  // the overall last nonzero
+    for (int32_t t = a.T - 1; t >= 0; --t)
+      if (rec[t].last >= 0) { L = (int64_t)t * kTE + rec[t].last; break; }
+    if (a.P - 1 - L > 0) total += glen((uint32_t)(a.P - L));  // trailing zero run
+    a.bits[ck] = (int64_t)total;
+    a.dist[ck] = rdist[0];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host side.
 // ---------------------------------------------------------------------------
@@ -2423,6 +2577,45 @@ int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream
   a.client_scale = client_scale;
   a.fsum_in = fsum_in;
   return decode_common(a, stream_buf, stream_off, stream_cap, idx, nclients, P, err, stream);
+}
+
+int64_t fc_vote_workspace_bytes(int32_t nclients, int64_t P, int32_t K) {
+  if (nclients <= 0 || P <= 0 || K <= 0) return 256;
+  return (int64_t)nclients * K * tiles_for(P) * (int64_t)sizeof(VoteRec);
+}
+
+int fc_vote_lengths(const float* const* xs, int32_t nclients, int64_t P, const float* steps, int32_t K,
+                    const int64_t* seeds, int mode, int64_t* bits, double* dist, void* workspace,
+                    int64_t workspace_bytes, void* stream) {
+  if (nclients <= 0 || K <= 0) return fail(-1, "nclients and K must be > 0");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
+  if (mode < 0 || mode > 2) return fail(-1, "mode must be 0 (uniform), 1 (stochastic) or 2 (dithered)");
+  if (!xs || !steps || !bits || !dist || (mode != FC_UNIFORM && !seeds)) return fail(-1, "null required pointer");
+  if (!workspace || workspace_bytes < fc_vote_workspace_bytes(nclients, P, K) || ((uintptr_t)workspace & 15))
+    return fail(-1, "workspace too small or misaligned");
+  VoteArgs a;
+  a.xs = xs;
+  a.nclients = nclients;
+  a.P = P;
+  a.T = (int32_t)tiles_for(P);
+  a.K = K;
+  a.steps = steps;
+  a.seeds = seeds;
+  a.rec = (VoteRec*)workspace;
+  a.bits = bits;
+  a.dist = dist;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t total = (int64_t)nclients * a.T;
+  const dim3 grid((unsigned)std::min<int64_t>(total, (int64_t)ncu * 16));
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == FC_UNIFORM) hipLaunchKernelGGL(k_vote_tiles<FC_UNIFORM>, grid, dim3(64), 0, s, a);
+  else if (mode == FC_STOCHASTIC) hipLaunchKernelGGL(k_vote_tiles<FC_STOCHASTIC>, grid, dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(k_vote_tiles<FC_DITHERED>, grid, dim3(64), 0, s, a);
+  if (hipGetLastError() != hipSuccess) return check_launch("k_vote_tiles");
+  hipLaunchKernelGGL(k_vote_finalize, dim3((unsigned)((int64_t)nclients * K)), dim3(256), 0, s, a);
+  return check_launch("k_vote_finalize");
 }
 
 int fc_dequantize(const int32_t* sum, int64_t P, float step, const float* noise_sum, float* out,

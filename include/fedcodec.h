@@ -26,6 +26,9 @@
  *   fc_decode_accumulate_scaled  QSGDFactory sum_encoded_value accumulate
  *                          (comparison_methods/qsgd.py:85-112): decode + per-client
  *                          dequantize(norm / num_steps) + float32 sum
+ *   fc_vote_lengths        QuantizeEncodeClientLambdaFactory vote_step_size: per
+ *                          option quantize + dequantize distortion + code length
+ *                          (quantize_encode_client_lambda.py:105-130), lengths only
  *   fc_noise_sum           federated_sum(noise) for dithered mode (quantize_encode.py:183)
  *   fc_client_norms        normalize_fn: mean_magnitude / max_magnitude /
  *                          dimensionless_norm (quantize_utils.py:20-29,
@@ -129,6 +132,16 @@ int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream
                                 const int64_t* stream_cap, const uint64_t* idx, int32_t nclients,
                                 int64_t P, const float* client_scale, const float* fsum_in,
                                 float* out, int32_t* err, void* stream);
+
+/* Step-size vote: for each client c and option k (steps = device float[K]),
+ * bits[c*K + k] = exact run-length-gamma code length (bits) of quantizing x_c
+ * with steps[k] (rounding `mode`, TF stream of seeds[c], the same draw for every
+ * option) and dist[c*K + k] = sum (x - dequantize(q))^2 (float64 accumulation
+ * of float32 tile partials).  Nothing is packed. */
+int64_t fc_vote_workspace_bytes(int32_t nclients, int64_t P, int32_t K);
+int fc_vote_lengths(const float* const* xs, int32_t nclients, int64_t P, const float* steps,
+                    int32_t K, const int64_t* seeds, int mode, int64_t* bits, double* dist,
+                    void* workspace, int64_t workspace_bytes, void* stream);
 
 /* out = (float(sum) [+ noise_sum]) * step (FTZ as TF-CPU). */
 int fc_dequantize(const int32_t* sum, int64_t P, float step, const float* noise_sum,

@@ -8,6 +8,7 @@ the C run-length-gamma restatement, for a list of client values:
 * ``stochastic_quantize_next`` aggregators/stochastic_quantize.py:57-88 (SumFactory inner)
 * ``one_bit_sgd_next``       aggregators/comparison_methods/one_bit_sgd.py:45-112
 * ``qsgd_next``              aggregators/comparison_methods/qsgd.py:62-146
+* ``client_lambda_next``     aggregators/quantize_encode_client_lambda.py:97-182
 
 Float reductions (distortion, 1-bit means, one-bit decoded sums) follow TF's
 float32 semantics up to summation order; tests compare them with tolerances.
@@ -141,3 +142,43 @@ def qsgd_next(client_values, num_steps, seeds):
       avg_distortion=F32(np.mean(dists)),
       avg_sparsity=F32(np.mean(sps)))
   return acc, measurements, codes
+
+
+def vote_step_size(x, options, lagrange_multiplier, rounding_type, seed):
+  """quantize_encode_client_lambda.py:105-130 for one client: (one-hot int32, losses)."""
+  x = np.asarray(x, np.float32).reshape(-1)
+  P = x.size
+  noise = qu.generate_noise(tuple(seed), P) if rounding_type == "dithered" else None
+  losses = []
+  for step in options:
+    step = F32(step)
+    q = _Q[rounding_type](x, step, tuple(seed))                                    # :114
+    deq = (qu.dithered_dequantize(q, step, noise) if rounding_type == "dithered"
+           else qu.uniform_dequantize(q, step))                                     # :115-116
+    d = qu.ftz(x) - deq
+    distortion = F32(F32(np.sum(d.astype(np.float64) ** 2)) / F32(P))              # :118-120
+    code, _ = codec.run_length_gamma_encode(q)
+    rate = F32(F32(codec.get_bitstring_length(code)) / F32(P))                      # :121-124
+    losses.append(F32(distortion + F32(lagrange_multiplier) * rate))                # :126
+  onehot = np.zeros(len(options), np.int32)
+  onehot[int(np.argmin(losses))] = 1                                                # :129-130
+  return onehot, np.array(losses, np.float32)
+
+
+def client_lambda_next(client_values, lagrange_multiplier, step_size, options,
+                       rounding_type="uniform", seeds=None, vote_seeds=None):
+  """QuantizeEncodeClientLambdaFactory round: (result, measurements, next_step)."""
+  xs = [np.asarray(v, np.float32).reshape(-1) for v in client_values]
+  if seeds is None:
+    seeds = [(c, c) for c in range(len(xs))]
+  if vote_seeds is None:
+    vote_seeds = seeds
+  result, _, _ = quantize_encode_next(xs, step_size, rounding_type, seeds=seeds)    # :152-159
+  counts = np.zeros(len(options), np.int32)
+  for c, x in enumerate(xs):
+    onehot, _ = vote_step_size(x, options, lagrange_multiplier, rounding_type, vote_seeds[c])
+    counts += onehot                                                                # :161-162
+  next_step = F32(np.asarray(options, np.float32)[int(np.argmax(counts))])           # :163-166
+  measurements = collections.OrderedDict(step_size=F32(step_size), step_size_options=list(options),
+                                         step_size_vote_counts=counts)
+  return result, measurements, next_step

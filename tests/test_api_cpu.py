@@ -128,3 +128,31 @@ def test_qsgd_create():
   assert process.initialize() == ()
   with pytest.raises(ValueError):  # qsgd_test.py:60-66
     qsgd.QSGDFactory(1.0).create((np.int32, (3,)))
+
+
+def test_client_lambda_create_and_builder():
+  from federated_amd.aggregators import quantize_encode_client_lambda as qecl  # pylint: disable=g-import-not-at-top
+  process = qecl.QuantizeEncodeClientLambdaFactory(1.0, 1.0, [0.5, 1.0, 2.0]).create(
+      (np.float32, (3,)))
+  state = process.initialize()
+  assert list(state.keys()) == ["step_size", "inner_state"] and state["step_size"] == 1.0
+  with pytest.raises(ValueError, match="rounding_type"):
+    qecl.QuantizeEncodeClientLambdaFactory(1.0, 1.0, [1.0], rounding_type="nearest")
+  with pytest.raises(ValueError):
+    qecl.QuantizeEncodeClientLambdaFactory(1.0, 1.0, [1.0]).create((np.int32, (3,)))
+  with pytest.raises(ValueError, match="step_size"):  # builder.py:562-565
+    builder.build_vote_step_size_aggregator(0.3)
+  with pytest.raises(ValueError, match="rounding_type"):
+    builder.build_vote_step_size_aggregator(0.5, rounding_type="x")
+  agg = builder.build_vote_step_size_aggregator(0.5)
+  inner = agg._inner  # pylint: disable=protected-access
+  assert inner._lagrange_multiplier == 0.03430265272  # pylint: disable=protected-access
+  opts = inner._step_size_options  # pylint: disable=protected-access
+  assert len(opts) == 7 and abs(opts[3] - 0.5) < 1e-12
+
+
+def test_vote_losses_and_ties():
+  from federated_amd.aggregators import quantize_encode_client_lambda as qecl  # pylint: disable=g-import-not-at-top
+  loss = qecl.vote_losses([[15, 9, 5]], [[0.0, 0.0, 3.0]], 3, 3, 1.0)
+  np.testing.assert_allclose(loss, [[16 / 3, 16 / 3, 1 + 8 / 3]], rtol=1e-6)
+  np.testing.assert_array_equal(qecl.votes_from_losses([[1.0, 1.0, 2.0]]), [[1, 0, 0]])  # first on ties

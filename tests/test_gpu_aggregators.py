@@ -229,3 +229,57 @@ def test_qsgd_codes_bit_exact(gpu):
                                         torch.from_numpy(seeds), _lib.STOCHASTIC, norms=steps)
   for c in range(C):
     assert batch.client_code(c) == codes[c]
+
+
+# quantize_encode_client_lambda_test.py:80-132
+def test_client_lambda_reference_execution(gpu):
+  from federated_amd.aggregators import quantize_encode_client_lambda as qecl  # pylint: disable=g-import-not-at-top
+  process = qecl.QuantizeEncodeClientLambdaFactory(1.0, 1.0, [0.5, 1.0, 2.0]).create(
+      (np.float32, (3,)))
+  out = process.next(process.initialize(), [np.ones(3, np.float32)] * 2)
+  np.testing.assert_array_equal(out.result, [2.0, 2.0, 2.0])
+  np.testing.assert_array_equal(out.measurements["step_size_vote_counts"], [0, 0, 2])
+  assert out.measurements["step_size"] == 1.0 and out.state["step_size"] == 2.0
+
+
+@pytest.mark.parametrize("rounding", ["uniform", "stochastic", "dithered"])
+@pytest.mark.parametrize("P,C", [(7, 2), (5000, 3), (200003, 4)])
+def test_vote_lengths_match_oracle(gpu, rounding, P, C):
+  """Per-option code lengths are exact; distortions within float tolerance."""
+  from oracle import codec as ocodec  # pylint: disable=g-import-not-at-top
+  from oracle import quantize_utils as oq  # pylint: disable=g-import-not-at-top
+  rng = np.random.default_rng(P * 3 + C)
+  xs = [(rng.standard_normal(P) * rng.uniform(0.05, 2)).astype(np.float32) for _ in range(C)]
+  xs[0][: P // 3] = 0.0  # long zero runs across tiles
+  options = [0.05, 0.1, 0.5, 1.0, 2.0, 7.0, 1e-3]
+  seeds = np.array([[3 + c, 11 * c] for c in range(C)], np.int64)
+  bits, dist = codec.vote_lengths([torch.from_numpy(x).to(gpu) for x in xs], options, seeds,
+                                  {"uniform": 0, "stochastic": 1, "dithered": 2}[rounding])
+  bits, dist = bits.cpu().numpy(), dist.cpu().numpy()
+  qfn = {"uniform": lambda x, s, sd: oq.uniform_quantize(x, s), "stochastic": oq.stochastic_quantize,
+         "dithered": oq.dithered_quantize}[rounding]
+  for c in range(C):
+    noise = oq.generate_noise(tuple(seeds[c]), P) if rounding == "dithered" else None
+    for k, step in enumerate(options):
+      q = qfn(xs[c], np.float32(step), tuple(seeds[c]))
+      assert bits[c, k] == ocodec.encoded_bits(q), (c, k)
+      deq = oq.dithered_dequantize(q, np.float32(step), noise) if noise is not None else \
+          oq.uniform_dequantize(q, np.float32(step))
+      want = np.sum((oq.ftz(xs[c]) - deq).astype(np.float64) ** 2)
+      np.testing.assert_allclose(dist[c, k], want, rtol=1e-5, atol=1e-12)
+
+
+def test_client_lambda_matches_oracle(gpu):
+  from federated_amd.aggregators import quantize_encode_client_lambda as qecl  # pylint: disable=g-import-not-at-top
+  rng = np.random.default_rng(21)
+  P, C = 3001, 6
+  xs = [rng.uniform(-1.0 / (c + 1), 1.0 / (c + 1), P).astype(np.float32) for c in range(C)]
+  options = [0.01, 0.1, 0.5, 1.0, 2.0]
+  seeds = np.array([[c, c + 1] for c in range(C)], np.int64)
+  process = qecl.QuantizeEncodeClientLambdaFactory(0.001, 0.5, options, "stochastic").create(
+      (np.float32, (P,)))
+  out = process.next(process.initialize(), xs, seeds=seeds)
+  want, m, next_step = oagg.client_lambda_next(xs, 0.001, 0.5, options, "stochastic", seeds=seeds)
+  np.testing.assert_array_equal(out.result, want)
+  np.testing.assert_array_equal(out.measurements["step_size_vote_counts"], m["step_size_vote_counts"])
+  assert out.state["step_size"] == next_step

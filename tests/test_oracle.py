@@ -226,3 +226,15 @@ def test_qsgd_different_clients_bounds():
   assert np.all(res - np.array([2.0 + hi, 4.0 + hi, 6.0 + hi]) <= 1e-6)
   assert m["avg_bitrate"] == np.float64(56.0 / 3.0)
   assert m["avg_distortion"] <= max(1.0 - lo, hi - 1.0) ** 2 / 2.0
+
+
+def test_client_lambda_known_answer():
+  # quantize_encode_client_lambda_test.py:80-132: options [0.5, 1, 2], lambda 1, two
+  # clients of ones(3): losses [16/3, 16/3, 1 + 8/3] -> both vote for 2.0
+  res, m, next_step = oagg.client_lambda_next([np.ones(3, np.float32)] * 2, 1.0, 1.0,
+                                              [0.5, 1.0, 2.0])
+  np.testing.assert_array_equal(res, [2.0, 2.0, 2.0])
+  np.testing.assert_array_equal(m["step_size_vote_counts"], [0, 0, 2])
+  assert next_step == 2.0 and m["step_size"] == 1.0
+  onehot, losses = oagg.vote_step_size(np.ones(3, np.float32), [0.5, 1.0, 2.0], 1.0, "uniform", (0, 0))
+  np.testing.assert_allclose(losses, [16 / 3, 16 / 3, 1 + 8 / 3], rtol=1e-6)
