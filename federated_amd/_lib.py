@@ -38,6 +38,8 @@ SIGNATURES = {
     "fc_client_norms": (_INT, [_P, _I32, _I64, _INT, _P, _P]),
     "fc_finalize": (_INT, [_P, _P, _I32, _I64, _P, _P, _P]),
     "fc_onebit_encode": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _P]),
+    "fc_drive_encode": (_INT, [_P, _I32, _I64, _INT, _P, _P, _P, _P]),
+    "fc_hadamard": (_INT, [_P, _I32, _I64, _INT, _I64, _I64, _P]),
     "fc_onebit_decode_sum": (_INT, [_P, _P, _I32, _I64, _P, _P]),
 }
 

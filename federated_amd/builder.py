@@ -26,6 +26,7 @@ HBM pass.  Parity of the wrappers with TFF is **unpinned** (TFF absent; no
 fixture in the reference holds their outputs).
 """
 import collections
+import inspect
 import math
 
 import numpy as np
@@ -35,10 +36,90 @@ from federated_amd import _lib
 from federated_amd import builder_configs
 from federated_amd import codec
 from federated_amd import tff_compat as tc
+from federated_amd.aggregators import _values
 from federated_amd.aggregators import quantize_encode
 from federated_amd.aggregators import quantize_encode_client_lambda
+from federated_amd.aggregators.comparison_methods import drive
+from federated_amd.aggregators.comparison_methods import one_bit_sgd
+from federated_amd.aggregators.comparison_methods import qsgd
 
 F32 = np.float32
+
+
+def _accepts(fn, name):
+  try:
+    return name in inspect.signature(fn).parameters
+  except (TypeError, ValueError):
+    return False
+
+
+def call_inner(process, state, rows, seeds=None, prescale=None):
+  """process.next(state, rows, ...) passing the optional seeds / fused pre-scales
+  only to processes that take them; otherwise the pre-scales (x * clip) * weight
+  are applied on the device first."""
+  kw = {}
+  if seeds is not None and _accepts(process.next, "seeds"):
+    kw["seeds"] = seeds
+  if prescale is not None:
+    if _accepts(process.next, "prescale"):
+      kw["prescale"] = prescale
+    else:
+      ps = np.asarray(prescale, np.float32).reshape(len(rows), 2)
+      rows = [(r * float(ps[c, 0])) * float(ps[c, 1]) for c, r in enumerate(rows)]
+  return process.next(state, rows, **kw)
+
+
+class HadamardTransformFactory(tc.UnweightedAggregationFactory):
+  """tff.aggregators.HadamardTransformFactory (builder.py:68-69) restated on MI355X.
+
+  Each client's flattened value is zero-padded to n = 2^k and rotated by
+  y = H D x / sqrt(n) (``fc_hadamard``: D = Rademacher signs of the round seed);
+  the inner factory aggregates the rotated values; the server applies the
+  inverse x = D H y / sqrt(n) to the aggregate and drops the padding.  The sign
+  stream and seed schedule of TFF's implementation are not available here:
+  parity unpinned (round-trip and linearity are tested).
+  """
+
+  def __init__(self, inner_agg_factory):
+    self._inner = inner_agg_factory
+
+  def create(self, value_type):
+    value_type = tc.to_type(value_type)
+    if not tc.is_structure_of_floats(value_type) or not value_type.is_tensor():
+      raise ValueError("Expect value_type to be a float tensor, found %s." % (value_type,))
+    shape = value_type.shape
+    P = value_type.num_elements
+    n = 1 << max(0, (P - 1).bit_length())
+    inner = self._inner.create(tc.TensorType(np.float32, (n,)))
+
+    def init_fn():
+      return collections.OrderedDict(round_seed=np.zeros(2, np.int64), inner_state=inner.initialize())
+
+    def next_fn(state, value, seeds=None, prescale=None, rotation_seed=None):
+      rows, vshape, host = _values.to_device_rows(value, torch.float32)
+      if vshape != shape:
+        raise ValueError("client value shape %s != %s" % (vshape, shape))
+      if prescale is not None:
+        ps = np.asarray(prescale, np.float32).reshape(len(rows), 2)
+        rows = [(r * float(ps[c, 0])) * float(ps[c, 1]) for c, r in enumerate(rows)]
+      if rotation_seed is None:
+        rotation_seed = quantize_encode.clock_seeds(1)[0]
+      rotation_seed = np.asarray(rotation_seed, np.int64).reshape(2)
+      padded = []
+      for r in rows:
+        t = torch.zeros(n, dtype=torch.float32, device=r.device)
+        t[:P] = r
+        padded.append(t)
+      codec.hadamard_(padded, rotation_seed)
+      out = call_inner(inner, state["inner_state"], padded, seeds=seeds)
+      res = torch.as_tensor(out.result).cuda().reshape(-1).to(torch.float32).contiguous()
+      codec.hadamard_([res], rotation_seed, inverse=True)
+      new_state = collections.OrderedDict(round_seed=rotation_seed, inner_state=out.state)
+      return tc.MeasuredProcessOutput(state=new_state,
+                                      result=_values.finish(res[:P].contiguous(), shape, host),
+                                      measurements=out.measurements)
+
+    return tc.AggregationProcess(init_fn, next_fn)
 
 
 class QuantileEstimate:
@@ -122,7 +203,7 @@ class WrappedAggregationFactory(tc.WeightedAggregationFactory):
         scale = (clip_norm * np.minimum(inv, F32(1.0) / clip_norm)).astype(np.float32)
         s0 = (s0 * scale).astype(np.float32)
       prescale = np.stack([s0, w], axis=1)
-      out = inner.next(state["inner_state"], rows, seeds=seeds, prescale=prescale)
+      out = call_inner(inner, state["inner_state"], rows, seeds=seeds, prescale=prescale)
       denom = F32(np.sum(w, dtype=np.float32)) if wrap._weighted else F32(C)
       res = torch.as_tensor(out.result).cuda().reshape(-1)
       res = res / denom if denom != 0 else torch.zeros_like(res)
@@ -149,10 +230,13 @@ def configure_aggregator(factory,
                          task: str = ""):
   """builder.py:37-119 (see module docstring for what is restated)."""
   del task
-  if rotation in ("hadamard", "dft"):
+  if rotation == "hadamard":
+    factory = HadamardTransformFactory(factory)
+  elif rotation == "dft":
     raise NotImplementedError(
-        "rotation=%r needs the TFF HadamardTransform/DFT factories (SURVEY.md 8f row 4)" % rotation)
-  if rotation != "identity":
+        "rotation='dft' (tff.aggregators.DiscreteFourierTransformFactory) is not restated; "
+        "'hadamard' and 'identity' are")
+  elif rotation != "identity":
     raise ValueError(
         "Provided `rotation` must be one of 'dft', 'hadamard' or 'identity'.")
   if group_layers:
@@ -229,5 +313,42 @@ def build_vote_step_size_aggregator(
   factory = quantize_encode_client_lambda.QuantizeEncodeClientLambdaFactory(
       lagrange_multiplier, step_size, step_size_options, rounding_type)
 
+  return configure_aggregator(factory, rotation, concatenate, zeroing, clipping,
+                              weighted)
+
+
+def build_drive_aggregator(
+    rotation: str = "hadamard",
+    concatenate: bool = True,
+    zeroing: bool = True,
+    clipping: bool = True,
+    weighted: bool = True):
+  """Creates an aggregation factory for comparing to DRIVE (builder.py:272-298)."""
+  factory = drive.DRIVEFactory()
+  return configure_aggregator(factory, rotation, concatenate, zeroing, clipping,
+                              weighted)
+
+
+def build_one_bit_sgd_aggregator(
+    rotation: str = "identity",
+    concatenate: bool = True,
+    zeroing: bool = True,
+    clipping: bool = True,
+    weighted: bool = True):
+  """Creates an aggregation factory for comparing to 1-bit SGD (builder.py:301-327)."""
+  factory = one_bit_sgd.OneBitSGDFactory()
+  return configure_aggregator(factory, rotation, concatenate, zeroing, clipping,
+                              weighted)
+
+
+def build_qsgd_aggregator(
+    num_steps: float,
+    rotation: str = "identity",
+    concatenate: bool = True,
+    zeroing: bool = True,
+    clipping: bool = True,
+    weighted: bool = True):
+  """Creates an aggregation factory for comparing to QSGD (builder.py:330-358)."""
+  factory = qsgd.QSGDFactory(num_steps=num_steps)
   return configure_aggregator(factory, rotation, concatenate, zeroing, clipping,
                               weighted)

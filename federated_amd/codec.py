@@ -292,3 +292,29 @@ def onebit_decode_sum(masks, means, nclients, P):
   _lib.call("fc_onebit_decode_sum", _lib.ptr(masks), _lib.ptr(means), int(nclients), int(P),
             _lib.ptr(out), _lib.stream_handle())
   return out
+
+
+def drive_encode(xs, min_distortion=False):
+  """DRIVE client encode: (masks, means=(-scale, +scale) per client, dist float64)."""
+  rows = _rows(xs, torch.float32)
+  P = rows[0].numel()
+  device = rows[0].device
+  C = len(rows)
+  ptrs = _ptr_array(rows, device)
+  nw = (P + 31) // 32
+  masks = torch.empty(C * nw, dtype=torch.int32, device=device)
+  means = torch.empty(2 * C, dtype=torch.float32, device=device)
+  dist = torch.empty(C, dtype=torch.float64, device=device)
+  _lib.call("fc_drive_encode", _lib.ptr(ptrs), C, P, int(bool(min_distortion)), _lib.ptr(masks),
+            _lib.ptr(means), _lib.ptr(dist), _lib.stream_handle())
+  return masks, means, dist
+
+
+def hadamard_(rows, seed, inverse=False):
+  """In-place randomized Hadamard transform of device rows of a power-of-two length."""
+  _lib.require_gpu()
+  n = rows[0].numel()
+  ptrs = _ptr_array(rows, rows[0].device)
+  _lib.call("fc_hadamard", _lib.ptr(ptrs), len(rows), n, int(bool(inverse)), int(seed[0]), int(seed[1]),
+            _lib.stream_handle())
+  return rows

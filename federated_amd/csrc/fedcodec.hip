@@ -2332,6 +2332,133 @@ __global__ __launch_bounds__(256) void k_vote_finalize(VoteArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// DRIVE (comparison_methods/drive.py:58-76): per client the sign mask (bit set
+// = non-negative), scale = ||x||_2^2 / ||x||_1 (unbiased, divide_no_nan) or
+// ||x||_1 / P (min_distortion) in float32 from float64 sums, and the
+// distortion sum (x - (+-scale))^2.  The server sum reuses k_onebit_decode_sum
+// with (below, above) = (-scale, +scale).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_drive_encode(const float* const* xs, int64_t P, int min_distortion,
+                                                           uint32_t* masks, float* means, double* dist) {
+  __shared__ double r0[kThreads], r1[kThreads];
+  __shared__ float scale_s;
+  const int c = blockIdx.x;
+  const float* x = xs[c];
+  const int64_t nw = (P + 31) / 32;
+  uint32_t* m = masks + (int64_t)c * nw;
+  double sa = 0, sq = 0;
+  for (int64_t w = threadIdx.x; w < nw; w += kThreads) {
+    uint32_t bits = 0;
+    for (int k = 0; k < 32; ++k) {
+      const int64_t i = w * 32 + k;
+      if (i >= P) break;
+      const float v = x[i] + 0.0f;  // DAZ
+      sa += fabs((double)v);
+      sq += (double)v * (double)v;
+      if (!(v < 0.0f)) bits |= 1u << k;  // mask_negatives = x < 0 (drive.py:59)
+    }
+    m[w] = bits;
+  }
+  r0[threadIdx.x] = sa;
+  r1[threadIdx.x] = sq;
+  __syncthreads();
+  for (int o = kThreads / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      r0[threadIdx.x] += r0[threadIdx.x + o];
+      r1[threadIdx.x] += r1[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float norm1 = (float)r0[0];
+    float scale;
+    if (min_distortion) {
+      scale = norm1 / (float)P;                       // drive.py:61-62
+    } else {
+      const float norm2 = (float)sqrt(r1[0]);
+      const float n2sq = norm2 * norm2;
+      scale = norm1 == 0.0f ? 0.0f : n2sq / norm1;     // drive.py:63-65 (divide_no_nan)
+    }
+    means[2 * c] = -scale;
+    means[2 * c + 1] = scale;
+    scale_s = scale;
+  }
+  __syncthreads();
+  const float sc = scale_s;
+  double dd = 0;
+  for (int64_t i = threadIdx.x; i < P; i += kThreads) {
+    const float v = x[i] + 0.0f;
+    const float dec = (v < 0.0f) ? -sc : sc;
+    const float e = v - dec;
+    dd += (double)(e * e);
+  }
+  r0[threadIdx.x] = dd;
+  __syncthreads();
+  for (int o = kThreads / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) r0[threadIdx.x] += r0[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dist[c] = r0[0];
+}
+
+// ---------------------------------------------------------------------------
+// Randomized Hadamard rotation (the TFF HadamardTransformFactory wrapper that
+// builder.py:68-71 puts around a codec): y = H D x / sqrt(n) on zero-padded
+// length n = 2^k, D = Rademacher signs drawn from Philox4x32-10 of the round
+// seed (element i: bit 31 of output word i % 4 of counter i / 4); the inverse
+// is x = D H y / sqrt(n).  One pass does up to 12 butterfly levels of a 4096-
+// element group in LDS: pass 0 covers levels 0..11 of contiguous blocks, later
+// passes levels L0..L0+k-1 of groups of C = 4096 / 2^k consecutive columns by
+// 2^k rows at stride 2^L0 (rows are C * 4 bytes contiguous).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float rademacher(const Key4& key, int64_t i) {
+  const uint4 r = philox_group(key, (uint32_t)(i >> 2));
+  const uint32_t w = (i & 3) == 0 ? r.x : (i & 3) == 1 ? r.y : (i & 3) == 2 ? r.z : r.w;
+  return (w >> 31) ? -1.0f : 1.0f;
+}
+
+__global__ __launch_bounds__(256) void k_fwht_pass(float* const* rows, int64_t n, int L0, int k, int sign_in,
+                                                   int sign_out, float scale, int64_t seed0, int64_t seed1) {
+  __shared__ float buf[4096];
+  const int64_t G = (int64_t)1 << k;               // rows of a group
+  const int64_t gsize = G * (L0 == 0 ? 1 : (4096 >> k));
+  const int64_t C = gsize >> k;                    // consecutive columns per group
+  const int64_t S = (int64_t)1 << L0;              // row stride
+  const int64_t per_row = n / gsize;               // groups per client row
+  const int64_t c = blockIdx.x / per_row;
+  const int64_t g = blockIdx.x - c * per_row;
+  const int64_t nblk = S / C;                      // column blocks below the levels
+  const int64_t hi = g / nblk, cb = g - hi * nblk;
+  const int64_t base = hi * (S << k) + cb * C;
+  float* x = rows[c];
+  const Key4 key = tf_seed_scramble(seed0, seed1);
+  for (int64_t t = threadIdx.x; t < gsize; t += 256) {
+    const int64_t e = base + (t / C) * S + (t % C);
+    float v = x[e];
+    if (sign_in) v *= rademacher(key, e);
+    buf[t] = v;
+  }
+  __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    const int64_t h = C << j;  // partner distance in buf
+    for (int64_t b = threadIdx.x; b < gsize / 2; b += 256) {
+      const int64_t lo = (b / h) * 2 * h + (b % h);
+      const float u = buf[lo], w = buf[lo + h];
+      buf[lo] = u + w;
+      buf[lo + h] = u - w;
+    }
+    __syncthreads();
+  }
+  for (int64_t t = threadIdx.x; t < gsize; t += 256) {
+    const int64_t e = base + (t / C) * S + (t % C);
+    float v = buf[t] * scale;
+    if (sign_out) v *= rademacher(key, e);
+    x[e] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host side.
 // ---------------------------------------------------------------------------
@@ -2616,6 +2743,38 @@ int fc_vote_lengths(const float* const* xs, int32_t nclients, int64_t P, const f
   if (hipGetLastError() != hipSuccess) return check_launch("k_vote_tiles");
   hipLaunchKernelGGL(k_vote_finalize, dim3((unsigned)((int64_t)nclients * K)), dim3(256), 0, s, a);
   return check_launch("k_vote_finalize");
+}
+
+int fc_drive_encode(const float* const* xs, int32_t nclients, int64_t P, int min_distortion, uint32_t* masks,
+                    float* means, double* dist, void* stream) {
+  if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
+  if (!xs || !masks || !means || !dist) return fail(-1, "null pointer");
+  hipLaunchKernelGGL(k_drive_encode, dim3(nclients), dim3(kThreads), 0, (hipStream_t)stream, xs, P,
+                     min_distortion, masks, means, dist);
+  return check_launch("k_drive_encode");
+}
+
+int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, int64_t seed0, int64_t seed1,
+                void* stream) {
+  if (nclients <= 0 || n <= 0 || (n & (n - 1)) || n > (1LL << 30)) return fail(-1, "n must be a power of two");
+  if (!rows) return fail(-1, "null pointer");
+  int levels = 0;
+  while ((1LL << levels) < n) ++levels;
+  const float scale = (float)(1.0 / std::sqrt((double)n));
+  hipStream_t s = (hipStream_t)stream;
+  int L0 = 0;
+  while (L0 < levels || (levels == 0 && L0 == 0)) {
+    const int k = L0 == 0 ? std::min(levels, 12) : std::min(levels - L0, 8);
+    const bool first = L0 == 0, last = L0 + k >= levels;
+    const int64_t gsize = (int64_t)1 << (L0 == 0 ? k : 12);
+    const int64_t groups = (int64_t)nclients * (n / gsize);
+    hipLaunchKernelGGL(k_fwht_pass, dim3((unsigned)groups), dim3(256), 0, s, rows, n, L0, k,
+                       (int)(first && !inverse), (int)(last && inverse), last ? scale : 1.0f, seed0, seed1);
+    if (hipGetLastError() != hipSuccess) return check_launch("k_fwht_pass");
+    if (levels == 0) break;
+    L0 += k;
+  }
+  return 0;
 }
 
 int fc_dequantize(const int32_t* sum, int64_t P, float step, const float* noise_sum, float* out,

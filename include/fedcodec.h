@@ -35,6 +35,10 @@
  *                          quantize_encode.py:79-90, 145)
  *   fc_finalize            avg_distortion / avg_sparsity / bit lengths per client
  *                          (quantize_encode.py:150-155, elias_gamma_encode.py:22-24, 100-108)
+ *   fc_drive_encode        DRIVEFactory encode (comparison_methods/drive.py:58-76); its
+ *                          server sum is fc_onebit_decode_sum with (-scale, +scale)
+ *   fc_hadamard            tff.aggregators.HadamardTransformFactory rotation that
+ *                          builder.py:68-71 wraps around a codec (randomized FWHT)
  *   fc_onebit_encode/_decode_sum  OneBitSGDFactory encode/decode_and_sum
  *                          (comparison_methods/one_bit_sgd.py:45-81, 87-112)
  *
@@ -169,6 +173,18 @@ int fc_onebit_encode(const float* const* xs, int32_t nclients, int64_t P, float 
                      uint32_t* masks, float* means, double* dist, void* stream);
 int fc_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t nclients,
                          int64_t P, float* out, void* stream);
+
+/* DRIVE: masks bit set = x >= 0 (not negative), means[2c] = -scale, means[2c+1] =
+ * +scale with scale = ||x||_2^2 / ||x||_1 (min_distortion = 0, divide_no_nan) or
+ * ||x||_1 / P (min_distortion = 1), dist[c] = sum (x - decode)^2. */
+int fc_drive_encode(const float* const* xs, int32_t nclients, int64_t P, int min_distortion,
+                    uint32_t* masks, float* means, double* dist, void* stream);
+
+/* In-place randomized Hadamard transform of nclients rows of n = 2^k floats:
+ * forward y = H D x / sqrt(n), inverse (inverse = 1) x = D H y / sqrt(n), with D
+ * the Rademacher signs of the Philox stream of (seed0, seed1). */
+int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, int64_t seed0,
+                int64_t seed1, void* stream);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,9 @@ the C run-length-gamma restatement, for a list of client values:
 * ``one_bit_sgd_next``       aggregators/comparison_methods/one_bit_sgd.py:45-112
 * ``qsgd_next``              aggregators/comparison_methods/qsgd.py:62-146
 * ``client_lambda_next``     aggregators/quantize_encode_client_lambda.py:97-182
+* ``drive_next``             aggregators/comparison_methods/drive.py:48-124
+* ``hadamard_forward/inverse`` the randomized Hadamard rotation builder.py:68-69 wraps
+  (tff.aggregators.HadamardTransformFactory; TFF absent: sign stream unpinned)
 
 Float reductions (distortion, 1-bit means, one-bit decoded sums) follow TF's
 float32 semantics up to summation order; tests compare them with tolerances.
@@ -182,3 +185,57 @@ def client_lambda_next(client_values, lagrange_multiplier, step_size, options,
   measurements = collections.OrderedDict(step_size=F32(step_size), step_size_options=list(options),
                                          step_size_vote_counts=counts)
   return result, measurements, next_step
+
+
+def drive_next(client_values, scaling_factor="unbiased"):
+  """DRIVEFactory round: (float32 result, measurements)."""
+  xs = [qu.ftz(np.asarray(v, np.float32).reshape(-1)) for v in client_values]
+  P = xs[0].size
+  acc = np.zeros(P, np.float32)
+  dists = []
+  for x in xs:
+    neg = x < F32(0.0)                                                         # :59
+    norm1 = F32(np.sum(np.abs(x).astype(np.float64)))
+    if scaling_factor == "min_distortion":
+      scale = F32(norm1 / F32(P))                                              # :61-62
+    else:
+      norm2 = F32(np.sqrt(np.sum(x.astype(np.float64) ** 2)))
+      sq = F32(norm2 * norm2)
+      scale = F32(0.0) if norm1 == 0 else F32(sq / norm1)                      # :63-65
+    dec = np.where(neg, -scale, scale).astype(np.float32)                      # :48-56
+    dists.append(F32(np.sum((x - dec).astype(np.float64) ** 2) / P))          # :69-70
+    acc = (acc + dec).astype(np.float32)                                       # :88-90
+  return acc, collections.OrderedDict(avg_bitrate=F32((F32(P) + F32(32.0)) / F32(P)),
+                                      avg_distortion=F32(np.mean(dists)))
+
+
+def rademacher(n, seed):
+  """Signs of the rotation: bit 31 of the Philox stream of `seed` (element i ->
+  output word i % 4 of counter i / 4), as fc_hadamard draws them."""
+  from oracle import philox  # pylint: disable=g-import-not-at-top
+  bits = philox.random_bits(n, tuple(seed))
+  return np.where(bits >> 31, F32(-1.0), F32(1.0)).astype(np.float32)
+
+
+def fwht(x):
+  """Unnormalised fast Walsh-Hadamard transform (float64) of a power-of-two vector."""
+  y = np.asarray(x, np.float64).copy()
+  h = 1
+  while h < y.size:
+    y = y.reshape(-1, 2, h)
+    y = np.stack([y[:, 0] + y[:, 1], y[:, 0] - y[:, 1]], axis=1).reshape(-1)
+    h *= 2
+  return y
+
+
+def hadamard_forward(x, seed):
+  x = np.asarray(x, np.float32).reshape(-1)
+  n = 1 << max(0, (x.size - 1).bit_length())
+  v = np.zeros(n, np.float32)
+  v[:x.size] = x
+  return fwht(v * rademacher(n, seed)) / np.sqrt(n)
+
+
+def hadamard_inverse(y, seed, P):
+  n = y.size
+  return (fwht(y) / np.sqrt(n) * rademacher(n, seed))[:P]

@@ -156,3 +156,20 @@ def test_vote_losses_and_ties():
   loss = qecl.vote_losses([[15, 9, 5]], [[0.0, 0.0, 3.0]], 3, 3, 1.0)
   np.testing.assert_allclose(loss, [[16 / 3, 16 / 3, 1 + 8 / 3]], rtol=1e-6)
   np.testing.assert_array_equal(qecl.votes_from_losses([[1.0, 1.0, 2.0]]), [[1, 0, 0]])  # first on ties
+
+
+def test_drive_create_and_builders():
+  from federated_amd.aggregators.comparison_methods import drive  # pylint: disable=g-import-not-at-top
+  with pytest.raises(ValueError, match="scaling_factor"):  # drive.py:36-38
+    drive.DRIVEFactory("biased")
+  with pytest.raises(ValueError):
+    drive.DRIVEFactory().create((np.int32, (3,)))
+  assert drive.DRIVEFactory().create((np.float32, (3,))).initialize() == ()
+  agg = builder.build_drive_aggregator()  # rotation defaults to hadamard (builder.py:272-273)
+  assert isinstance(agg._inner, builder.HadamardTransformFactory)  # pylint: disable=protected-access
+  from federated_amd.aggregators.comparison_methods import qsgd  # pylint: disable=g-import-not-at-top
+  assert isinstance(builder.build_qsgd_aggregator(7.0)._inner, qsgd.QSGDFactory)  # pylint: disable=protected-access
+  with pytest.raises(NotImplementedError):
+    builder.build_drive_aggregator(rotation="dft")
+  with pytest.raises(ValueError):
+    builder.build_one_bit_sgd_aggregator(rotation="fft")

@@ -283,3 +283,60 @@ def test_client_lambda_matches_oracle(gpu):
   np.testing.assert_array_equal(out.result, want)
   np.testing.assert_array_equal(out.measurements["step_size_vote_counts"], m["step_size_vote_counts"])
   assert out.state["step_size"] == next_step
+
+
+@pytest.mark.parametrize("values,scaling,want,dist", [
+    ([[-1.0, 0.0, 2.0]] * 2, "min_distortion", [-2.0, 2.0, 2.0], 2. / 3.),
+    ([[1.0, -1.0, 0.0], [0.0, 0.0, 0.0]], "min_distortion", [2. / 3., -2. / 3., 2. / 3.], 1. / 9.),
+    ([[1.0, 1.0, 1.0]], "unbiased", [1.0, 1.0, 1.0], 0.0),
+    ([[-1.0, 0.0, 2.0]] * 2, "unbiased", [-10. / 3., 10. / 3., 10. / 3.], 10. / 9.),
+    ([[1.0, -1.0, 0.0], [0.0, 0.0, 0.0]], "unbiased", [1.0, -1.0, 1.0], 1. / 6.),
+])
+def test_drive_reference_execution(gpu, values, scaling, want, dist):
+  from federated_amd.aggregators.comparison_methods import drive  # pylint: disable=g-import-not-at-top
+  process = drive.DRIVEFactory(scaling).create((np.float32, (3,)))
+  out = process.next(process.initialize(), [np.asarray(v, np.float32) for v in values])
+  np.testing.assert_allclose(out.result, want, rtol=1e-6)
+  np.testing.assert_allclose(out.measurements["avg_distortion"], dist, rtol=1e-6)
+  np.testing.assert_allclose(out.measurements["avg_bitrate"], 35.0 / 3.0, rtol=1e-6)
+
+
+@pytest.mark.parametrize("scaling", ["unbiased", "min_distortion"])
+def test_drive_matches_oracle(gpu, scaling):
+  from federated_amd.aggregators.comparison_methods import drive  # pylint: disable=g-import-not-at-top
+  rng = np.random.default_rng(4)
+  P, C = 100003, 5
+  xs = [(rng.standard_normal(P) * (c + 0.5)).astype(np.float32) for c in range(C)]
+  out = drive.DRIVEFactory(scaling).create((np.float32, (P,))).next((), xs)
+  want, m = oagg.drive_next(xs, scaling)
+  np.testing.assert_allclose(out.result, want, rtol=1e-5, atol=1e-5)
+  np.testing.assert_allclose(out.measurements["avg_distortion"], m["avg_distortion"], rtol=1e-5)
+
+
+@pytest.mark.parametrize("P", [1, 3, 4096, 5000, 1 << 17, 300001])
+def test_hadamard_matches_oracle_and_round_trips(gpu, P):
+  rng = np.random.default_rng(P)
+  x = rng.standard_normal(P).astype(np.float32)
+  n = 1 << max(0, (P - 1).bit_length())
+  t = torch.zeros(n, dtype=torch.float32, device=gpu)
+  t[:P] = torch.from_numpy(x).to(gpu)
+  codec.hadamard_([t], (7, 9))
+  y = t.cpu().numpy()
+  want = oagg.hadamard_forward(x, (7, 9))
+  np.testing.assert_allclose(y, want, rtol=1e-4, atol=1e-5 * max(1.0, np.sqrt(np.log2(n))))
+  codec.hadamard_([t], (7, 9), inverse=True)
+  np.testing.assert_allclose(t.cpu().numpy()[:P], x, rtol=1e-4, atol=1e-5)
+
+
+def test_drive_with_hadamard_rotation_end_to_end(gpu):
+  rng = np.random.default_rng(8)
+  P, C = 5000, 4
+  xs = [(rng.standard_normal(P) * 0.01).astype(np.float32) for _ in range(C)]
+  agg = builder.build_drive_aggregator(zeroing=False, clipping=False, weighted=False)
+  process = agg.create((np.float32, (P,)))
+  out = process.next(process.initialize(), xs)
+  res = np.asarray(out.result)
+  assert res.shape == (P,)
+  # unweighted mean of the clients, approximated by 1-bit DRIVE in the rotated basis
+  mean = np.mean(np.stack(xs), axis=0)
+  assert np.linalg.norm(res - mean) < np.linalg.norm(mean) * 1.5

@@ -238,3 +238,27 @@ def test_client_lambda_known_answer():
   assert next_step == 2.0 and m["step_size"] == 1.0
   onehot, losses = oagg.vote_step_size(np.ones(3, np.float32), [0.5, 1.0, 2.0], 1.0, "uniform", (0, 0))
   np.testing.assert_allclose(losses, [16 / 3, 16 / 3, 1 + 8 / 3], rtol=1e-6)
+
+
+# drive_test.py:92-201 known answers
+@pytest.mark.parametrize("values,scaling,want,dist", [
+    ([[-1.0, 0.0, 2.0]] * 2, "min_distortion", [-2.0, 2.0, 2.0], 2. / 3.),
+    ([[1.0, -1.0, 0.0], [0.0, 0.0, 0.0]], "min_distortion", [2. / 3., -2. / 3., 2. / 3.], 1. / 9.),
+    ([[1.0, 1.0, 1.0]], "unbiased", [1.0, 1.0, 1.0], 0.0),
+    ([[-1.0, 0.0, 2.0]] * 2, "unbiased", [-10. / 3., 10. / 3., 10. / 3.], 10. / 9.),
+    ([[1.0, -1.0, 0.0], [0.0, 0.0, 0.0]], "unbiased", [1.0, -1.0, 1.0], 1. / 6.),
+])
+def test_drive_known_answers(values, scaling, want, dist):
+  res, m = oagg.drive_next(values, scaling)
+  np.testing.assert_allclose(res, want, rtol=1e-6)
+  np.testing.assert_allclose(m["avg_distortion"], dist, rtol=1e-6)
+  np.testing.assert_allclose(m["avg_bitrate"], 35.0 / 3.0, rtol=1e-6)
+
+
+def test_hadamard_oracle_is_orthonormal():
+  rng = np.random.default_rng(1)
+  for P in (1, 3, 4, 1000, 4097):
+    x = rng.standard_normal(P).astype(np.float32)
+    y = oagg.hadamard_forward(x, (5, 6))
+    np.testing.assert_allclose(np.linalg.norm(y), np.linalg.norm(x), rtol=1e-6)
+    np.testing.assert_allclose(oagg.hadamard_inverse(y, (5, 6), P), x, atol=1e-6)
