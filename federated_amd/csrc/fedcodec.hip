@@ -1803,16 +1803,22 @@ struct SegReader {
   }
 };
 
-// Decode table: the next 12 window bits -> up to two complete codes.
-//   [3:0] L1  bits of code 1 (0: code 1 is longer than 12 bits)
-//   [7:4] L   bits of both codes (= L1 when only one fits)
-//   [12:8] d1   [18:13] v1 + 32   [23:19] d2   [29:24] v2 + 32   [31:30] n codes
+// Decode table: the next 12 window bits -> up to two complete codes, as two
+// words laid out for the fast step (decode_segment) -- every field comes out
+// with one AND, one constant shift or none:
+//   x: [7:0] 4*d1 (byte offset of code 1 from the previous nonzero)
+//      [31:24] 4*d2 (0 when only one code fits)
+//   y: [5:0] L = bits of the decoded codes (0: code 1 is longer than 12 bits)
+//      [13:8] L1 = bits of code 1  [14] two codes
+//      [23:16] v1 (int8)  [31:24] v2 (int8, 0 when only one code fits)
 constexpr int kLutBits = 12;
 constexpr int kLutSize = 1 << kLutBits;
 
-__device__ __forceinline__ uint32_t lut_entry(uint32_t x) {
-  uint32_t top = x << (32 - kLutBits);
-  uint32_t used = 0, n = 0, e = 0;
+__device__ __forceinline__ uint2 lut_entry(uint32_t i) {
+  uint32_t top = i << (32 - kLutBits);
+  uint32_t used = 0, n = 0, L1 = 0;
+  uint32_t d[2] = {0, 0};
+  int32_t v[2] = {0, 0};
   for (int c = 0; c < 2; ++c) {
     const uint32_t z1 = (uint32_t)__clz(top);
     if (z1 > 4) break;
@@ -1822,16 +1828,19 @@ __device__ __forceinline__ uint32_t lut_entry(uint32_t x) {
     if (z2 > 4) break;
     const uint32_t L = 2u * (z1 + z2) + 3u;
     if (used + L > (uint32_t)kLutBits) break;
-    const uint32_t d = top >> (sa + 1u);
+    d[c] = top >> (sa + 1u);
     const uint32_t m = rest >> (31u - 2u * z2);
-    const int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
+    v[c] = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
     used += L;
-    if (c == 0) e |= L | (d << 8) | ((uint32_t)(v + 32) << 13);
-    else e |= (d << 19) | ((uint32_t)(v + 32) << 24);
+    if (c == 0) L1 = L;
     ++n;
     top <<= L;
   }
-  return e | (used << 4) | (n << 30);
+  uint2 e;
+  e.x = (4u * d[0]) | ((4u * d[1]) << 24);
+  e.y = used | (L1 << 8) | ((n == 2 ? 1u : 0u) << 14) | (((uint32_t)v[0] & 0xFFu) << 16) |
+        ((uint32_t)v[1] << 24);
+  return e;
 }
 
 // One segment = one client's code for one 1024-element tile: bits [b0, b1),
@@ -1849,88 +1858,116 @@ __device__ __forceinline__ void acc_add(int32_t* my, uint32_t i, int32_t v, floa
   else atomicAdd(my + i, v);
 }
 
+typedef __attribute__((address_space(3))) int32_t* lds_iptr;
+typedef __attribute__((address_space(3))) float* lds_fptr;
+
+// Accumulator add at LDS byte address a: int32 client sum, or (QSGD) the
+// float32 sum of each client's dequantised value f32(v) * scale.
 template <bool FACC>
-__device__ __forceinline__ uint32_t table_step(uint32_t e, int32_t rem, int32_t& rel, int32_t* my,
-                                               uint32_t& bad, float scale) {
-  const uint32_t L1 = e & 15u, L2 = (e >> 4) & 15u;
-  const bool two = (e >> 30) == 2u && (int32_t)L2 <= rem;  // a second code past the segment is not ours
-  const int32_t rel1 = rel + (int32_t)((e >> 8) & 31u);
-  const int32_t rel2 = rel1 + (int32_t)((e >> 19) & 31u);
-  const int32_t v1 = (int32_t)((e >> 13) & 63u) - 32;
-  const int32_t v2 = two ? (int32_t)((e >> 24) & 63u) - 32 : 0;
-  rel = two ? rel2 : rel1;
-  bad |= (uint32_t)rel >= (uint32_t)kTE;
-  acc_add<FACC>(my, min((uint32_t)rel1, (uint32_t)kTE - 1), v1, scale);
-  if (!FACC || v2 != 0) acc_add<FACC>(my, min((uint32_t)rel, (uint32_t)kTE - 1), v2, scale);
-  return two ? L2 : L1;
+__device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, float scale) {
+  // (a no-op zero add may point outside the accumulator -- harmless for int32;
+  // skipped for float, where it could quiet a NaN bit pattern of a table word)
+  if (FACC) {
+    if (v != 0) atomicAdd((float*)(lds_fptr)(uintptr_t)a, (float)v * scale);
+  } else {
+    atomicAdd((int32_t*)(lds_iptr)(uintptr_t)a, v);
+  }
 }
 
 // One segment = one client's code for one 1024-element tile: bits [b0, b1),
-// previous nonzero at tile-relative position rel.  Each iteration makes two
-// steps and one window refill: step A looks up the next 12 window bits (one or
-// two short codes) or decodes a longer code arithmetically from the top 32 bits
-// (longer than 32 bits: slow_code, then the reader restarts); step B is a
-// table step when >= 12 bits remain in the window.  Segments are < 2^31 bits.
+// previous nonzero at tile-relative position rel.  The accumulator position is
+// kept as an LDS byte address.  Far from the segment end (>= 24 bits left) an
+// iteration makes two unchecked table steps -- a code longer than 12 bits has
+// an all-zero entry, so such a step adds 0 and consumes nothing -- and then, if
+// neither step moved, decodes the long code arithmetically from the top 32
+// window bits (longer than 32 bits: slow_code, then the reader restarts).  Near
+// the end, steps check that a second code does not belong to the next tile.
+// The window always holds >= 33 valid bits when an iteration starts.
 template <bool FACC>
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
-                                               uint64_t b1, int32_t rel, int32_t* my,
-                                               const uint32_t* lut, int32_t* err, float scale) {
+                                               uint64_t b1, int32_t rel, uint32_t my_addr,
+                                               const uint2* lut, int32_t* err, float scale) {
   SegReader r;
   r.init(base, cap, b0);
   int32_t rem = (int32_t)(b1 - b0);
+  uint32_t relb = my_addr + 4u * (uint32_t)rel;  // byte address of the previous nonzero's slot
+  const uint32_t lo_addr = my_addr, hi_addr = my_addr + 4u * (uint32_t)kTE;
   uint32_t bad = 0;
   while (rem > 0) {
-    uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
-    uint32_t L;
-    if (e & 15u) {
-      L = table_step<FACC>(e, rem, rel, my, bad, scale);
-      r.win <<= L;
-      r.nwin -= (int32_t)L;
-    } else {
-      const uint32_t top = (uint32_t)(r.win >> 32);
-      const uint32_t z1 = (uint32_t)__clz(top);
-      const uint32_t sa = 30u - 2u * z1;        // sign-bit position
-      const uint32_t rest = top << (32u - sa);  // bits after the sign bit
-      const uint32_t z2 = (uint32_t)__clz(rest);
-      L = 2u * (z1 + z2) + 3u;
-      uint32_t d = top >> (sa + 1u);
-      const uint32_t m = rest >> (31u - 2u * z2);
-      int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
-      if (L <= 32u) {
-        r.win <<= L;
-        r.nwin -= (int32_t)L;
-      } else {  // a code longer than 32 bits (or a malformed one)
-        const uint64_t pos = b1 - (uint64_t)rem;
-        const CodeVal cv = slow_code(base, cap, pos);
-        if (cv.L == 0) {
-          bad = 1;
-          break;
-        }
-        L = cv.L;
-        d = cv.d;
-        v = cv.v;
-        r.init(base, cap, pos + L);
-      }
-      rel += (int32_t)d;
-      bad |= (uint32_t)rel >= (uint32_t)kTE;
-      acc_add<FACC>(my, min((uint32_t)rel, (uint32_t)kTE - 1), v, scale);
-    }
-    rem -= (int32_t)L;
+    uint32_t moved = 1;
+    const bool far = rem >= 24;
+    if (far) {
 #pragma unroll
-    for (int st = 1; st < FC_DEC_STEPS; ++st) {
-      e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
-      if (rem > 0 && r.nwin >= kLutBits && (e & 15u)) {
-        L = table_step<FACC>(e, rem, rel, my, bad, scale);
+      for (int st = 0; st < 2; ++st) {
+        const uint2 e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+        relb += e.x & 0xFFu;
+        acc_add_at<FACC>(relb, ((int32_t)(e.y << 8)) >> 24, scale);
+        relb += e.x >> 24;
+        acc_add_at<FACC>(relb, ((int32_t)e.y) >> 24, scale);
+        const uint32_t L = e.y & 63u;
         r.win <<= L;
         r.nwin -= (int32_t)L;
         rem -= (int32_t)L;
+        moved = st == 0 ? L : (moved | L);
       }
+    }
+    if (rem > 0 && (!far || moved == 0)) {  // right after a refill, or nothing consumed
+      const uint2 e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+      uint32_t L = e.y & 63u;
+      if (L != 0) {  // near the end: a second code past the segment is not ours
+        const uint32_t L1 = (e.y >> 8) & 63u;
+        const bool two = ((e.y >> 14) & 1u) && (int32_t)L <= rem;
+        relb += e.x & 0xFFu;
+        acc_add_at<FACC>(relb, ((int32_t)(e.y << 8)) >> 24, scale);
+        if (two) {
+          relb += e.x >> 24;
+          acc_add_at<FACC>(relb, ((int32_t)e.y) >> 24, scale);
+        } else {
+          L = L1;
+        }
+        r.win <<= L;
+        r.nwin -= (int32_t)L;
+      } else {  // a code longer than 12 bits
+        const uint32_t top = (uint32_t)(r.win >> 32);
+        const uint32_t z1 = (uint32_t)__clz(top);
+        const uint32_t sa = 30u - 2u * z1;        // sign-bit position
+        const uint32_t rest = top << (32u - sa);  // bits after the sign bit
+        const uint32_t z2 = (uint32_t)__clz(rest);
+        L = 2u * (z1 + z2) + 3u;
+        uint32_t d = top >> (sa + 1u);
+        const uint32_t m = rest >> (31u - 2u * z2);
+        int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
+        if (L <= 32u) {
+          r.win <<= L;
+          r.nwin -= (int32_t)L;
+        } else {  // a code longer than 32 bits (or a malformed one)
+          const uint64_t pos = b1 - (uint64_t)rem;
+          const CodeVal cv = slow_code(base, cap, pos);
+          if (cv.L == 0) {
+            bad = 1;
+            break;
+          }
+          L = cv.L;
+          d = cv.d;
+          v = cv.v;
+          r.init(base, cap, pos + L);
+        }
+        // the run may come from far before the tile: bound it before scaling to bytes
+        const int32_t rel_now = ((int32_t)(relb - my_addr)) >> 2;
+        const uint32_t rel_new = (uint32_t)(rel_now + (int32_t)d);
+        bad |= rel_new >= (uint32_t)kTE ? 1u : 0u;
+        relb = my_addr + 4u * min(rel_new, (uint32_t)kTE - 1);
+        acc_add_at<FACC>(relb, v, scale);
+      }
+      rem -= (int32_t)L;
     }
     if (r.nwin <= 32) {
       r.win |= (uint64_t)r.pop32() << (32 - r.nwin);
       r.nwin += 32;
     }
   }
+  // every decoded value must have landed inside this tile's accumulator
+  bad |= (relb < lo_addr || relb >= hi_addr) ? 1u : 0u;
   if (bad || rem != 0) atomicOr(err, 1);
 }
 
@@ -1939,15 +1976,15 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 // clients' values in LDS and writing the tile's sum / dequantised values.
 template <bool FACC>
 __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
-  extern __shared__ int32_t smem[];  // [kLutSize] table, then [tiles_per_wg][kTE] sums
-  uint32_t* lut = (uint32_t*)smem;
-  int32_t* acc = smem + kLutSize;
+  extern __shared__ int32_t smem[];  // [kLutSize] uint2 table, then [tiles_per_wg][kTE] sums
+  uint2* lut = (uint2*)smem;
+  int32_t* acc = smem + 2 * kLutSize;
   const int tid = threadIdx.x;
   const int tiles_per_wg = kThreads / a.lanes_per_tile;
   for (int i = tid; i < kLutSize; i += kThreads) lut[i] = lut_entry((uint32_t)i);
   const int sub = tid / a.lanes_per_tile;
   const int l = tid - sub * a.lanes_per_tile;
-  int32_t* my = acc + sub * kTE;
+  const uint32_t my_addr = (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * kTE);
   const int64_t ngroups = (a.T + tiles_per_wg - 1) / tiles_per_wg;
   for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int64_t t0 = grp * tiles_per_wg;
@@ -1962,7 +1999,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
         const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
         if (bend <= bstart) continue;
         const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
-        decode_segment<FACC>(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart, bend, rel, my, lut, a.err,
+        decode_segment<FACC>(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart, bend, rel, my_addr, lut, a.err,
                               FACC ? a.client_scale[c] : 0.0f);
       }
     }
@@ -2606,7 +2643,7 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   const bool facc = a.client_scale != nullptr;
   void (*kern)(DecodeArgs) = facc ? k_decode<true> : k_decode<false>;
   const int tpw = kThreads / lpt;
-  const size_t lds = (size_t)kLutSize * 4 + (size_t)tpw * kTE * sizeof(int32_t);
+  const size_t lds = (size_t)kLutSize * 8 + (size_t)tpw * kTE * sizeof(int32_t);
   int dev = 0, ncu = 256, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
