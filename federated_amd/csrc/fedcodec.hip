@@ -50,6 +50,10 @@ constexpr uint32_t kNoPos = 0x1FFF; // "no nonzero" in a 13-bit tile-relative fi
 // (MI355X_MICROARCH.md "dequeue"), so tickets come from kTicketShards counters,
 // one 64-B line each; stream k hands out tickets k, k + K, k + 2K, ... in order.
 constexpr int kTicketShards = 32;
+#ifndef FC_LOOKBACK_WIN
+#define FC_LOOKBACK_WIN 64
+#endif
+constexpr int kLookbackWin = FC_LOOKBACK_WIN;  // statuses prefetched for the vector look-back
 constexpr int kShardStride = 16;  // uint32 words between counters (64 B)
 
 // ---------------------------------------------------------------------------
@@ -92,15 +96,17 @@ __device__ __forceinline__ void philox10_ukey(uint32_t& c0, uint32_t& c1, uint32
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t kk0 = __builtin_amdgcn_readfirstlane(k0), kk1 = __builtin_amdgcn_readfirstlane(k1);
+    // round keys recomputed on the scalar unit at each use (volatile: not hoisted
+    // across chunks, where 20 live key SGPRs would spill into VGPR lanes)
+    uint32_t kk0, kk1;
+    asm volatile("s_add_u32 %0, %1, %2" : "=s"(kk0) : "s"(k0), "i"(0x9E3779B9u * (uint32_t)r));
+    asm volatile("s_add_u32 %0, %1, %2" : "=s"(kk1) : "s"(k1), "i"(0xBB67AE85u * (uint32_t)r));
     const uint32_t n0 = r < 2 ? (uint32_t)(p1 >> 32) ^ c1 ^ kk0 : xor3_vvs((uint32_t)(p1 >> 32), c1, kk0);
     const uint32_t n2 = r < 2 ? (uint32_t)(p0 >> 32) ^ c3 ^ kk1 : xor3_vvs((uint32_t)(p0 >> 32), c3, kk1);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;
     c2 = n2;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
   }
 }
 
@@ -474,20 +480,22 @@ __device__ unsigned long long g_stamps[16];
 __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t, int lane,
                                             uint32_t* spin_err, bool& slow, uint64_t pre1,
                                             uint64_t pre2) {
-  const int64_t ti = (int64_t)t - 64 + lane;
-  uint64_t w1 = kFlagPre, w2 = kFlagPre;  // ti < 0: virtual root prefix (last = -1, body 0)
-  bool valid = ti < 0;
-  if (!valid) {
-    w1 = pre1;
-    w2 = pre2;
-    valid = (w1 >> 62) != 0 && (w1 >> 62) == (w2 >> 62);
+  // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
+  // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
+  const int32_t ti = t - 64 + lane;
+  uint32_t h1 = (uint32_t)(pre1 >> 32), l1 = (uint32_t)pre1, h2 = (uint32_t)(pre2 >> 32), l2 = (uint32_t)pre2;
+  if (ti < 0) {
+    h1 = h2 = 0x80000000u;
+    l1 = l2 = 0u;
   }
+  // a status is readable once both granules carry the same nonzero flag
+  bool valid = h1 >= 0x40000000u && (h1 ^ h2) < 0x40000000u;
   uint32_t spins = 0;
   int p;
   for (;;) {
-    const uint64_t pre = __ballot(valid && (w1 >> 62) >= 2);
+    const uint64_t pre = __ballot(valid && h1 >= 0x80000000u);  // inclusive prefix (or slow)
     const uint64_t val = __ballot(valid);
-    if (pre == 0) {  // no prefix within 64 tiles: scalar walk
+    if (pre == 0) {  // no prefix in the window: scalar walk
       FC_COUNT(10, 1);
       return lookback(status_c, t, lane, spin_err, slow);
     }
@@ -504,48 +512,51 @@ __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t,
       return r;
     }
     if (!valid) {
-      w1 = ld_agent(status_c + 2 * ti);
-      w2 = ld_agent(status_c + 2 * ti + 1);
-      valid = (w1 >> 62) != 0 && (w1 >> 62) == (w2 >> 62);
+      const uint64_t w1 = ld_agent(status_c + 2 * (int64_t)ti);
+      const uint64_t w2 = ld_agent(status_c + 2 * (int64_t)ti + 1);
+      h1 = (uint32_t)(w1 >> 32);
+      l1 = (uint32_t)w1;
+      h2 = (uint32_t)(w2 >> 32);
+      l2 = (uint32_t)w2;
+      valid = h1 >= 0x40000000u && (h1 ^ h2) < 0x40000000u;
     }
   }
-  const uint32_t w1hi = (uint32_t)(w1 >> 32);
-  if ((__builtin_amdgcn_readlane(w1hi, p) >> 30) == 3u) {  // a slow tile: give up
+  const uint32_t ph = __builtin_amdgcn_readlane(h1, p);
+  if (ph >= 0xC0000000u) {  // a slow tile: give up
     slow = true;
     return seg_identity();
   }
   Seg r;
   r.has_nz = 1;
   r.first = -1;
+  // prefix at lane p: [61:36] last + 1, [35:0] bits
+  const int32_t plast = (int32_t)((ph >> 4) & ((1u << 26) - 1)) - 1;
+  const uint64_t pbody = ((uint64_t)(ph & 0xFu) << 32) | __builtin_amdgcn_readlane(l1, p);
   FC_COUNT(8, 1);
   FC_COUNT(13, 63 - p);
   if (p == 63) {  // the predecessor's own inclusive prefix
     FC_COUNT(12, 1);
-    r.last = (int32_t)((__builtin_amdgcn_readlane(w1hi, 63) >> 4) & ((1u << 26) - 1)) - 1;
-    r.body = ((uint64_t)(__builtin_amdgcn_readlane(w1hi, 63) & 0xFu) << 32) |
-             __builtin_amdgcn_readlane((uint32_t)w1, 63);
-    r.tail = __builtin_amdgcn_readlane((uint32_t)w2, 63);
+    r.last = plast;
+    r.body = pbody;
+    r.tail = __builtin_amdgcn_readlane(l2, 63);
     return r;
   }
-  // per-lane decode: prefix lane p, aggregates above it, nothing below
+  // aggregates above the prefix: [61:49] first_rel, [48:36] last_rel, body < 2^32
   const bool agg = lane > p;
-  const uint32_t fr = (uint32_t)(w1 >> 49) & 0x1FFF, lr = (uint32_t)(w1 >> 36) & 0x1FFF;
+  const uint32_t fr = (h1 >> 17) & 0x1FFFu, lr = (h1 >> 4) & 0x1FFFu;
   const bool nz = agg && fr != kNoPos;
-  const int32_t tb = (int32_t)(ti * kTE);
-  int32_t lastv = -1;
-  if (lane == p) lastv = (int32_t)((w1 >> 36) & ((1u << 26) - 1)) - 1;
-  if (nz) lastv = tb + (int32_t)lr;
+  const int32_t tb = ti * kTE;
+  int32_t lastv = agg ? -1 : (lane == p ? plast : -1);
+  lastv = nz ? tb + (int32_t)lr : lastv;
   const int32_t M = dpp_incl_max(lastv);
   const int32_t Mx = dpp_shr1(M, -1);  // last nonzero before this tile
-  const uint32_t abody = (uint32_t)(w1 & kMask36);
-  uint32_t contrib = agg ? abody : 0u;
+  uint32_t contrib = agg ? l1 : 0u;
   if (nz) contrib += glen((uint32_t)(tb + (int32_t)fr - Mx));
   const uint32_t csum = (uint32_t)wave_sum_i((int32_t)contrib);
   r.last = lane63(M);
-  r.body = (((uint64_t)(__builtin_amdgcn_readlane(w1hi, p) & 0xFu) << 32) |
-            __builtin_amdgcn_readlane((uint32_t)w1, p)) + csum;
-  if (__builtin_amdgcn_readlane(abody, 63) >= 32u) {
-    r.tail = __builtin_amdgcn_readlane((uint32_t)w2, 63);
+  r.body = pbody + csum;
+  if (__builtin_amdgcn_readlane(l1, 63) >= 32u) {  // the newest body holds the last 32 bits
+    r.tail = __builtin_amdgcn_readlane(l2, 63);
     return r;
   }
   FC_COUNT(11, 1);
@@ -653,7 +664,11 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
                                                      float& dist, int32_t& nnz, const uint32_t* clut,
                                                      int32_t nvalid = 4) {
   uint4 rb = make_uint4(0, 0, 0, 0);
-  if (MODE != FC_UNIFORM) rb = philox_group_u(cq.key, g);
+  if (FC_ABL & 8) {  // diagnostics: a cheap hash instead of Philox
+    rb.x = g * 2654435761u; rb.y = rb.x ^ 0x9E3779B9u; rb.z = rb.x + cq.key.k0; rb.w = rb.y ^ cq.key.k1;
+  } else if (MODE != FC_UNIFORM) {
+    rb = philox_group_u(cq.key, g);
+  }
   const uint32_t rbits[4] = {rb.x, rb.y, rb.z, rb.w};
   float q[4];
   bool nz[4];
@@ -1146,8 +1161,11 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
     if (ticket1 < total_tiles && lane == 0) ntk = atomicAdd(my_counter, 1u);  // ticket after next
     // the pending tile's look-back window (lane i: tile pt-64+i), fetched now and
     // used after this tile's work
-    uint64_t pw1 = kFlagPre, pw2 = kFlagPre;
-    if (!(FC_ABL & 16) && pv && pt + lane >= 64) {
+    uint64_t pw1 = 0, pw2 = 0;  // not fetched: unreadable (lookback_vec re-polls it if needed)
+    // only the kLookbackWin nearest statuses are fetched: with C clients and W waves
+    // about W / C tiles of a client are in flight, so the nearest inclusive prefix is
+    // rarely further back (lookback_vec falls back to the scalar walk when it is)
+    if (!(FC_ABL & 16) && pv && pt + lane >= 64 && lane >= 64 - kLookbackWin) {
       const uint64_t* sp = a.status + 2 * ((int64_t)pc * a.T + pt - 64 + lane);
       pw1 = ld_agent(sp);
       pw2 = ld_agent(sp + 1);
@@ -1259,7 +1277,10 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
       const uint64_t lngmask = __ballot(lng != 0);
       // ---- C: emit the lane's run code and chunks (codes past the window land in
       //      the guard words; the tile is then slow)
-      {
+      if (FC_ABL & 1) {  // diagnostics: no emission
+        asm volatile("" :: "v"(dv), "v"(R), "v"((uint32_t)cacc[0]), "v"((uint32_t)cacc[1]), "v"((uint32_t)cacc[2]),
+                     "v"((uint32_t)cacc[3]), "v"(is));
+      } else {
         uint32_t o = kPre + is - ltot;
         emit32(win, dv, R, o);
         o += R;
@@ -1351,6 +1372,12 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         excl.first = excl.last = -1;
       } else {
         excl = lookback_vec(a.status + 2 * (int64_t)pc * a.T, pt, lane, a.spin_err, slow, pw1, pw2);
+        if (FC_ABL & 4096) {  // diagnostics: the look-back runs, its result is dropped
+          asm volatile("" :: "s"((uint32_t)excl.body), "s"(excl.last), "s"(excl.tail));
+          excl = seg_identity();
+          excl.has_nz = 1;
+          excl.first = excl.last = -1;
+        }
       }
       if (slow) {
         if (lane == 0) {
@@ -1870,7 +1897,14 @@ __device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, float scale) {
   if (FACC) {
     if (v != 0) atomicAdd((float*)(lds_fptr)(uintptr_t)a, (float)v * scale);
   } else {
+#if FC_DEC_ABL & 1
+    a = (a & ~127u) | ((threadIdx.x & 31u) << 2);  // diagnostics: every lane its own bank
+#endif
+#if FC_DEC_ABL & 2
+    asm volatile("" :: "v"(a), "v"(v));  // diagnostics: no accumulation
+#else
     atomicAdd((int32_t*)(lds_iptr)(uintptr_t)a, v);
+#endif
   }
 }
 
