@@ -63,6 +63,16 @@ constexpr int kIters = 4096;
 #define A_MBCNT(x, y) asm volatile("v_mbcnt_lo_u32_b32 %0, -1, %0" : "+v"(x));
 #define A_DSOR(x, y) asm volatile("ds_or_b32 %0, %1" :: "v"(x & 0xFFCu), "v"(y) : "memory");
 #define A_DSREAD(x, y) asm volatile("ds_read_b32 %0, %1" : "=v"(x) : "v"(y & 0x3FCu) : "memory");
+
+#define A_ADDSDWA(x, y) asm volatile("v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "+v"(x) : "v"(y));
+#define A_MOVSDWA(x, y) asm volatile("v_mov_b32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(x) : "v"(y));
+#define A_BFEI(x, y) asm volatile("v_bfe_i32 %0, %0, 16, 8" : "+v"(x));
+#define A_ASHR(x, y) asm volatile("v_ashrrev_i32 %0, 24, %0" : "+v"(x));
+#define A_AND(x, y) asm volatile("v_and_b32 %0, %0, %1" : "+v"(x) : "v"(y));
+#define A_SUB(x, y) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(x) : "v"(y));
+#define A_MIN(x, y) asm volatile("v_min_u32 %0, %0, %1" : "+v"(x) : "v"(y));
+#define A_LSHLADD(x, y) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(x) : "v"(y));
+#define A_ADD3(x, y) asm volatile("v_add3_u32 %0, %0, %1, %0" : "+v"(x) : "v"(y));
 K(k_mad, A_MAD)
 K(k_mulhi, A_MULHI)
 K(k_mullo, A_MULLO)
@@ -76,6 +86,15 @@ K(k_cvt, A_CVT)
 K(k_floor, A_FLOOR)
 K(k_dpp, A_DPP)
 K(k_pkfma, A_PKFMA)
+K(k_addsdwa, A_ADDSDWA)
+K(k_movsdwa, A_MOVSDWA)
+K(k_bfei, A_BFEI)
+K(k_ashr, A_ASHR)
+K(k_and, A_AND)
+K(k_sub, A_SUB)
+K(k_min, A_MIN)
+K(k_lshladd, A_LSHLADD)
+K(k_add3, A_ADD3)
 K(k_cnd64, A_CND64)
 K(k_cmp, A_CMP)
 K(k_cmpcnd, A_CMPCND)
@@ -109,12 +128,12 @@ int main() {
       {"v_mul_u32_u24", k_mul24}, {"v_add_u32", k_add}, {"v_bitop3_b32", k_xor3},
       {"v_fma_f32", k_fma}, {"v_lshlrev_b64", k_shl64}, {"v_cndmask_b32", k_cndmask},
       {"v_cvt_f32_u32", k_cvt}, {"v_floor_f32", k_floor}, {"v_add_u32_dpp", k_dpp},
-      {"v_pk_fma_f32", k_pkfma}, {"CND64", k_cnd64}, {"CMP", k_cmp}, {"CMPCND", k_cmpcnd}, {"LSHLOR", k_lshlor}, {"ALIGNBIT", k_alignbit}, {"BFE", k_bfe}, {"FFBH", k_ffbh}, {"MAX3", k_max3}, {"CVTI", k_cvti}, {"MULF", k_mulf}, {"ANDOR", k_andor}, {"LSHLADD64", k_lshladd64}, {"MOV", k_mov}, {"MAXDPP", k_maxdpp}, {"CEIL", k_ceil}, {"RNDNE", k_rndne}, {"LSHL32", k_lshl32}, {"WRITELANE", k_writelane}, {"READLANE", k_readlane}, {"MBCNT", k_mbcnt}};
+      {"v_pk_fma_f32", k_pkfma}, {"ADDSDWA", k_addsdwa}, {"MOVSDWA", k_movsdwa}, {"BFEI", k_bfei}, {"ASHR", k_ashr}, {"AND", k_and}, {"SUB", k_sub}, {"MIN", k_min}, {"LSHLADD", k_lshladd}, {"ADD3", k_add3}, {"CND64", k_cnd64}, {"CMP", k_cmp}, {"CMPCND", k_cmpcnd}, {"LSHLOR", k_lshlor}, {"ALIGNBIT", k_alignbit}, {"BFE", k_bfe}, {"FFBH", k_ffbh}, {"MAX3", k_max3}, {"CVTI", k_cvti}, {"MULF", k_mulf}, {"ANDOR", k_andor}, {"LSHLADD64", k_lshladd64}, {"MOV", k_mov}, {"MAXDPP", k_maxdpp}, {"CEIL", k_ceil}, {"RNDNE", k_rndne}, {"LSHL32", k_lshl32}, {"WRITELANE", k_writelane}, {"READLANE", k_readlane}, {"MBCNT", k_mbcnt}};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   printf("CUs %d, clock %d MHz (nominal)\n", ncu, clk_khz / 1000);
-  for (int wps : {4, 8}) {  // waves per SIMD
+  for (int wps : {8}) {  // waves per SIMD
     const int blocks = ncu * 4 * wps;
     for (auto& k : ks) {
       hipLaunchKernelGGL(k.k, dim3(blocks), dim3(64), 0, 0, out, 1u);
