@@ -1830,22 +1830,17 @@ struct SegReader {
   }
 };
 
-// Decode table: the next 12 window bits -> up to two complete codes, as two
-// words laid out for the fast step (decode_segment) -- every field comes out
-// with one AND, one constant shift or none:
-//   x: [7:0] 4*d1 (byte offset of code 1 from the previous nonzero)
-//      [31:24] 4*d2 (0 when only one code fits)
-//   y: [5:0] L = bits of the decoded codes (0: code 1 is longer than 12 bits)
-//      [13:8] L1 = bits of code 1  [14] two codes
-//      [23:16] v1 (int8)  [31:24] v2 (int8, 0 when only one code fits)
+// Decode table: the next 12 window bits -> up to two complete codes in one
+// 32-bit word, every field out with one AND or a constant shift pair:
+//   [6:0] 4*d1   [13:7] 4*d2 (0: one code)   [19:14] v1   [25:20] v2 (6-bit
+//   two's complement, 0: one code)   [29:26] L = bits of the decoded codes
+//   (0: the first code is longer than 12 bits -- the entry is then all zero)
 constexpr int kLutBits = 12;
 constexpr int kLutSize = 1 << kLutBits;
 
-__device__ __forceinline__ uint2 lut_entry(uint32_t i) {
+__device__ __forceinline__ uint32_t lut_entry(uint32_t i) {
   uint32_t top = i << (32 - kLutBits);
-  uint32_t used = 0, n = 0, L1 = 0;
-  uint32_t d[2] = {0, 0};
-  int32_t v[2] = {0, 0};
+  uint32_t used = 0, e = 0;
   for (int c = 0; c < 2; ++c) {
     const uint32_t z1 = (uint32_t)__clz(top);
     if (z1 > 4) break;
@@ -1855,34 +1850,14 @@ __device__ __forceinline__ uint2 lut_entry(uint32_t i) {
     if (z2 > 4) break;
     const uint32_t L = 2u * (z1 + z2) + 3u;
     if (used + L > (uint32_t)kLutBits) break;
-    d[c] = top >> (sa + 1u);
+    const uint32_t d = top >> (sa + 1u);
     const uint32_t m = rest >> (31u - 2u * z2);
-    v[c] = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
+    const int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
     used += L;
-    if (c == 0) L1 = L;
-    ++n;
+    e |= ((4u * d) << (7 * c)) | (((uint32_t)v & 63u) << (14 + 6 * c));
     top <<= L;
   }
-  uint2 e;
-  e.x = (4u * d[0]) | ((4u * d[1]) << 24);
-  e.y = used | (L1 << 8) | ((n == 2 ? 1u : 0u) << 14) | (((uint32_t)v[0] & 0xFFu) << 16) |
-        ((uint32_t)v[1] << 24);
-  return e;
-}
-
-// One segment = one client's code for one 1024-element tile: bits [b0, b1),
-// previous nonzero at tile-relative position rel.  Each step looks up the next
-// 12 window bits (one or two short codes); a code longer than 12 bits is
-// decoded arithmetically from the top 32 window bits, one longer than 32 bits
-// by slow_code (the reader then restarts after it).
-// One table step: up to two codes from the next 12 window bits (caller checked
-// e & 15 != 0, i.e. the first code fits).  Returns the bits consumed.
-// Accumulator add: int32 client sum, or (QSGD) the float32 sum of each client's
-// dequantised value f32(v) * scale.
-template <bool FACC>
-__device__ __forceinline__ void acc_add(int32_t* my, uint32_t i, int32_t v, float scale) {
-  if (FACC) atomicAdd((float*)my + i, (float)v * scale);
-  else atomicAdd(my + i, v);
+  return used ? (e | (used << 26)) : 0u;
 }
 
 typedef __attribute__((address_space(3))) int32_t* lds_iptr;
@@ -1920,7 +1895,7 @@ __device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, float scale) {
 template <bool FACC>
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
                                                uint64_t b1, int32_t rel, uint32_t my_addr,
-                                               const uint2* lut, int32_t* err, float scale) {
+                                               const uint32_t* lut, int32_t* err, float scale) {
   SegReader r;
   r.init(base, cap, b0);
   int32_t rem = (int32_t)(b1 - b0);
@@ -1930,69 +1905,54 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
   while (rem > 0) {
     uint32_t moved = 1;
     const bool far = rem >= 24;
-    if (far) {
+    if (far) {  // two unchecked table steps (the window holds >= 33 bits, the segment >= 24)
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
-        const uint2 e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
-        relb += e.x & 0xFFu;
-        acc_add_at<FACC>(relb, ((int32_t)(e.y << 8)) >> 24, scale);
-        relb += e.x >> 24;
-        acc_add_at<FACC>(relb, ((int32_t)e.y) >> 24, scale);
-        const uint32_t L = e.y & 63u;
+        const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+        relb += e & 0x7Fu;
+        acc_add_at<FACC>(relb, ((int32_t)(e << 12)) >> 26, scale);
+        relb += (e >> 7) & 0x7Fu;
+        acc_add_at<FACC>(relb, ((int32_t)(e << 6)) >> 26, scale);
+        const uint32_t L = e >> 26;
         r.win <<= L;
         r.nwin -= (int32_t)L;
         rem -= (int32_t)L;
         moved = st == 0 ? L : (moved | L);
       }
     }
-    if (rem > 0 && (!far || moved == 0)) {  // right after a refill, or nothing consumed
-      const uint2 e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
-      uint32_t L = e.y & 63u;
-      if (L != 0) {  // near the end: a second code past the segment is not ours
-        const uint32_t L1 = (e.y >> 8) & 63u;
-        const bool two = ((e.y >> 14) & 1u) && (int32_t)L <= rem;
-        relb += e.x & 0xFFu;
-        acc_add_at<FACC>(relb, ((int32_t)(e.y << 8)) >> 24, scale);
-        if (two) {
-          relb += e.x >> 24;
-          acc_add_at<FACC>(relb, ((int32_t)e.y) >> 24, scale);
-        } else {
-          L = L1;
-        }
+    if (rem > 0 && (!far || moved == 0)) {
+      // right after a refill (>= 33 window bits): one code decoded arithmetically --
+      // near the segment end, or a code longer than 12 bits
+      const uint32_t top = (uint32_t)(r.win >> 32);
+      const uint32_t z1 = (uint32_t)__clz(top);
+      const uint32_t sa = 30u - 2u * z1;        // sign-bit position
+      const uint32_t rest = top << (32u - sa);  // bits after the sign bit
+      const uint32_t z2 = (uint32_t)__clz(rest);
+      uint32_t L = 2u * (z1 + z2) + 3u;
+      uint32_t d = top >> (sa + 1u);
+      const uint32_t m = rest >> (31u - 2u * z2);
+      int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
+      if (L <= 32u) {
         r.win <<= L;
         r.nwin -= (int32_t)L;
-      } else {  // a code longer than 12 bits
-        const uint32_t top = (uint32_t)(r.win >> 32);
-        const uint32_t z1 = (uint32_t)__clz(top);
-        const uint32_t sa = 30u - 2u * z1;        // sign-bit position
-        const uint32_t rest = top << (32u - sa);  // bits after the sign bit
-        const uint32_t z2 = (uint32_t)__clz(rest);
-        L = 2u * (z1 + z2) + 3u;
-        uint32_t d = top >> (sa + 1u);
-        const uint32_t m = rest >> (31u - 2u * z2);
-        int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
-        if (L <= 32u) {
-          r.win <<= L;
-          r.nwin -= (int32_t)L;
-        } else {  // a code longer than 32 bits (or a malformed one)
-          const uint64_t pos = b1 - (uint64_t)rem;
-          const CodeVal cv = slow_code(base, cap, pos);
-          if (cv.L == 0) {
-            bad = 1;
-            break;
-          }
-          L = cv.L;
-          d = cv.d;
-          v = cv.v;
-          r.init(base, cap, pos + L);
+      } else {  // a code longer than 32 bits (or a malformed one)
+        const uint64_t pos = b1 - (uint64_t)rem;
+        const CodeVal cv = slow_code(base, cap, pos);
+        if (cv.L == 0) {
+          bad = 1;
+          break;
         }
-        // the run may come from far before the tile: bound it before scaling to bytes
-        const int32_t rel_now = ((int32_t)(relb - my_addr)) >> 2;
-        const uint32_t rel_new = (uint32_t)(rel_now + (int32_t)d);
-        bad |= rel_new >= (uint32_t)kTE ? 1u : 0u;
-        relb = my_addr + 4u * min(rel_new, (uint32_t)kTE - 1);
-        acc_add_at<FACC>(relb, v, scale);
+        L = cv.L;
+        d = cv.d;
+        v = cv.v;
+        r.init(base, cap, pos + L);
       }
+      // the run may come from far before the tile: bound it before scaling to bytes
+      const int32_t rel_now = ((int32_t)(relb - my_addr)) >> 2;
+      const uint32_t rel_new = (uint32_t)(rel_now + (int32_t)d);
+      bad |= rel_new >= (uint32_t)kTE ? 1u : 0u;
+      relb = my_addr + 4u * min(rel_new, (uint32_t)kTE - 1);
+      acc_add_at<FACC>(relb, v, scale);
       rem -= (int32_t)L;
     }
     if (r.nwin <= 32) {
@@ -2010,9 +1970,9 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 // clients' values in LDS and writing the tile's sum / dequantised values.
 template <bool FACC>
 __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
-  extern __shared__ int32_t smem[];  // [kLutSize] uint2 table, then [tiles_per_wg][kTE] sums
-  uint2* lut = (uint2*)smem;
-  int32_t* acc = smem + 2 * kLutSize;
+  extern __shared__ int32_t smem[];  // [kLutSize] table, then [tiles_per_wg][kTE] sums
+  uint32_t* lut = (uint32_t*)smem;
+  int32_t* acc = smem + kLutSize;
   const int tid = threadIdx.x;
   const int tiles_per_wg = kThreads / a.lanes_per_tile;
   for (int i = tid; i < kLutSize; i += kThreads) lut[i] = lut_entry((uint32_t)i);
@@ -2677,7 +2637,7 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   const bool facc = a.client_scale != nullptr;
   void (*kern)(DecodeArgs) = facc ? k_decode<true> : k_decode<false>;
   const int tpw = kThreads / lpt;
-  const size_t lds = (size_t)kLutSize * 8 + (size_t)tpw * kTE * sizeof(int32_t);
+  const size_t lds = (size_t)kLutSize * 4 + (size_t)tpw * kTE * sizeof(int32_t);
   int dev = 0, ncu = 256, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
