@@ -1756,56 +1756,69 @@ __device__ __noinline__ CodeVal slow_code(const uint8_t* base, int64_t cap, uint
   return r;
 }
 
-// One segment = one client's code for one 1024-element tile: bits [b0, b1),
-// previous nonzero at tile-relative position rel.  Bit reader: a 64-bit window
-// (MSB-aligned, > 32 valid bits), a 128-bit reservoir behind it and the next
-// 16-byte block already in flight.  Codes that fit the top 32 window bits are
-// decoded branch-free; longer ones go through slow_code and the reader
-// restarts after them.
+// Bit reader of one segment: a 64-bit window (MSB-aligned, > 32 valid bits), a
+// 128-bit reservoir behind it, the rest of the current chunk (kDecChunk 16-byte
+// blocks, read by one lane at once) and the next chunk, requested at a batch
+// point.  Whole chunks: a lane's 16-byte reads of one line, spread over many
+// iterations, let the XCD's L2 (fewer lines than concurrent lane streams)
+// evict the line between reads -- measured 2.7x the code bytes fetched with
+// 16-byte reads.  Loads are issued only at batch points the wave reaches
+// together every kDecBatch iterations, so the wave's in-order memory counter
+// does not make a lane wait for loads other lanes issued an iteration ago.
 #ifndef FC_DEC_ABL
-#define FC_DEC_ABL 0  // decoder ablation bits (diagnostics only): 1 no LDS sums, 2 no table reads
+#define FC_DEC_ABL 0  // decoder ablation bits (diagnostics only): 1 sums one bank per lane, 2 no sums, 4 table reads one bank per lane
 #endif
-#ifndef FC_DEC_STEPS
-#define FC_DEC_STEPS 3  // decode steps per window refill (2: 3.47 ms, 3: 3.23, 4: 3.51 at C=1024, P=6M)
+#ifndef FC_DEC_BATCH
+#define FC_DEC_BATCH 4
 #endif
-#ifndef FC_DEC_BLOCKS
-#define FC_DEC_BLOCKS 1
+#ifndef FC_DEC_CHUNK
+#define FC_DEC_CHUNK 1
 #endif
-// Blocks of 16 B fetched per lane at once.  4 (one 64-B chunk) makes each line
-// a single L2 request even when the concurrent lane streams outnumber L2 lines,
-// but measured slower (block shuffling, fewer waves): 6.5 vs 4.2 ms at C=1024,
-// P=6M, so the reader fetches one 16-B block ahead.
-constexpr int kDecBlocks = FC_DEC_BLOCKS;
+constexpr int kDecBatch = FC_DEC_BATCH;  // decode iterations between batch points (power of 2)
+constexpr int kDecChunk = FC_DEC_CHUNK;  // 16-byte blocks per chunk (one 64-B line half at 4)
+#ifndef FC_DEC_LONG
+#define FC_DEC_LONG 4
+#endif
+constexpr int kDecLong = FC_DEC_LONG;  // iterations between arithmetic-decode slots (power of 2)
 struct SegReader {
   const uint4* p;
   const uint4* end;
-  uint4 nxt[kDecBlocks];       // next chunk (in flight)
-  uint4 cur[kDecBlocks - 1 > 0 ? kDecBlocks - 1 : 1];  // rest of the current chunk
-  int32_t cb;                  // blocks left in cur
+  uint4 cur[kDecChunk > 1 ? kDecChunk - 1 : 1];  // rest of the current chunk
+  uint4 nxt[kDecChunk];                          // next chunk (requested)
+  int32_t cb;                                    // blocks left in cur
+  uint32_t nv;                                   // nxt holds a chunk not yet taken
   uint64_t win, rh, rl;
   int32_t nwin, rb;
-  __device__ __forceinline__ void fetch() {
+  __device__ __forceinline__ void load_chunk(uint4* dst) {
 #pragma unroll
-    for (int i = 0; i < kDecBlocks; ++i) nxt[i] = *(p + i < end ? p + i : end - 1);  // clamped, unconditional
-    p += kDecBlocks;
+    for (int i = 0; i < kDecChunk; ++i) dst[i] = *(p + i < end ? p + i : end - 1);  // clamped
+    p += kDecChunk;
+  }
+  __device__ __forceinline__ void set_res(uint4 blk) {
+    rh = ((uint64_t)bswap32(blk.x) << 32) | bswap32(blk.y);
+    rl = ((uint64_t)bswap32(blk.z) << 32) | bswap32(blk.w);
+    rb = 128;
   }
   __device__ __forceinline__ void take_block() {
-    uint4 b;
-    if (kDecBlocks == 1 || cb == 0) {
-      b = nxt[0];
+    if (kDecChunk > 1 && cb > 0) {
+      set_res(cur[0]);
 #pragma unroll
-      for (int i = 0; i + 1 < kDecBlocks; ++i) cur[i] = nxt[i + 1];
-      cb = kDecBlocks - 1;
-      fetch();
-    } else {
-      b = cur[0];
-#pragma unroll
-      for (int i = 0; i + 2 < kDecBlocks; ++i) cur[i] = cur[i + 1];
+      for (int i = 0; i + 2 < kDecChunk; ++i) cur[i] = cur[i + 1];
       --cb;
+      return;
     }
-    rh = ((uint64_t)bswap32(b.x) << 32) | bswap32(b.y);
-    rl = ((uint64_t)bswap32(b.z) << 32) | bswap32(b.w);
-    rb = 128;
+    if (!nv) load_chunk(nxt);  // segment start, restart after a long code, or a lane far ahead
+    nv = 0;
+    set_res(nxt[0]);
+#pragma unroll
+    for (int i = 0; i + 1 < kDecChunk; ++i) cur[i] = nxt[i + 1];
+    cb = kDecChunk - 1;
+  }
+  __device__ __forceinline__ void batch() {
+    if (!nv) {
+      load_chunk(nxt);
+      nv = 1;
+    }
   }
   __device__ __forceinline__ uint32_t pop32() {
     const uint32_t w = (uint32_t)(rh >> 32);
@@ -1816,17 +1829,18 @@ struct SegReader {
     return w;
   }
   __device__ __forceinline__ void init(const uint8_t* base, int64_t cap, uint64_t bit) {
-    p = (const uint4*)base + (bit >> 7);
+    p = (const uint4*)base + ((bit >> 7) & ~(uint64_t)(kDecChunk - 1));  // chunk-aligned
     end = (const uint4*)base + (cap >> 4);
+    nv = 0;
     cb = 0;
-    fetch();
     take_block();
-    for (int i = (int)((bit >> 5) & 3); i > 0; --i) (void)pop32();
+    for (int i = (int)((bit >> 5) & (4 * kDecChunk - 1)); i > 0; --i) (void)pop32();
     win = (uint64_t)pop32() << 32;
     win |= pop32();
     const int skip = (int)(bit & 31);
     win <<= skip;
     nwin = 64 - skip;
+    batch();
   }
 };
 
@@ -1885,42 +1899,54 @@ __device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, float scale) {
 
 // One segment = one client's code for one 1024-element tile: bits [b0, b1),
 // previous nonzero at tile-relative position rel.  The accumulator position is
-// kept as an LDS byte address.  Far from the segment end (>= 24 bits left) an
-// iteration makes two unchecked table steps -- a code longer than 12 bits has
-// an all-zero entry, so such a step adds 0 and consumes nothing -- and then, if
-// neither step moved, decodes the long code arithmetically from the top 32
-// window bits (longer than 32 bits: slow_code, then the reader restarts).  Near
-// the end, steps check that a second code does not belong to the next tile.
-// The window always holds >= 33 valid bits when an iteration starts.
+// kept as an LDS byte address.  An iteration makes two table steps, each taking
+// the entry's codes only when they end inside the segment -- a code longer than
+// 12 bits has an all-zero entry, so such a step adds 0 and consumes nothing --
+// and a lane that took nothing decodes one code arithmetically from the top 32
+// window bits in the next arithmetic slot (longer than 32 bits: slow_code, then
+// the reader restarts).  The window holds >= 33 valid bits when an iteration
+// starts.
 template <bool FACC>
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
                                                uint64_t b1, int32_t rel, uint32_t my_addr,
                                                const uint32_t* lut, int32_t* err, float scale) {
   SegReader r;
   r.init(base, cap, b0);
-  int32_t rem = (int32_t)(b1 - b0);
+  // one running count of consumed bits: the segment end and the window refill
+  // compare against it (fill = cons + valid window bits)
+  const int32_t total = (int32_t)(b1 - b0);
+  int32_t cons = 0;
+  int32_t fill = r.nwin;
   uint32_t relb = my_addr + 4u * (uint32_t)rel;  // byte address of the previous nonzero's slot
   const uint32_t lo_addr = my_addr, hi_addr = my_addr + 4u * (uint32_t)kTE;
   uint32_t bad = 0;
-  while (rem > 0) {
-    uint32_t moved = 1;
-    const bool far = rem >= 24;
-    if (far) {  // two unchecked table steps (the window holds >= 33 bits, the segment >= 24)
+  uint32_t it = 0;
+  while (cons < total) {
+    if ((++it & (kDecBatch - 1)) == 0) r.batch();  // every active lane is on the same iteration
+    uint32_t moved = 0;
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
-        relb += e & 0x7Fu;
-        acc_add_at<FACC>(relb, ((int32_t)(e << 12)) >> 26, scale);
-        relb += (e >> 7) & 0x7Fu;
-        acc_add_at<FACC>(relb, ((int32_t)(e << 6)) >> 26, scale);
-        const uint32_t L = e >> 26;
-        r.win <<= L;
-        r.nwin -= (int32_t)L;
-        rem -= (int32_t)L;
-        moved = st == 0 ? L : (moved | L);
-      }
+    for (int st = 0; st < 2; ++st) {  // two table steps (the window holds >= 33 bits)
+#if FC_DEC_ABL & 4  // diagnostics: conflict-free table reads (every lane its own bank; wrong codes)
+      uint32_t e = lut[((uint32_t)(r.win >> 58) << 6) | (threadIdx.x & 63u)];
+#else
+      uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+#endif
+      // codes past the segment end belong to the client's next tile: such an entry is dropped
+      e = (e >> 26) <= (uint32_t)(total - cons) ? e : 0u;
+      relb += e & 0x7Fu;
+      acc_add_at<FACC>(relb, ((int32_t)(e << 12)) >> 26, scale);
+      relb += (e >> 7) & 0x7Fu;
+      acc_add_at<FACC>(relb, ((int32_t)(e << 6)) >> 26, scale);
+      const uint32_t L = e >> 26;
+      r.win <<= L;
+      cons += (int32_t)L;
+      if (st == 0) moved = L;  // a zero first step leaves the window as it was: so does the second
     }
-    if (rem > 0 && (!far || moved == 0)) {
+    // A lane whose table steps took nothing (a code longer than 12 bits, or a code
+    // pair running past the segment end) decodes one code arithmetically -- only on
+    // every kDecLong-th iteration, so the wave runs that block rarely instead of
+    // whenever any of its 64 lanes needs it; the lane idles meanwhile.
+    if (moved == 0 && (it & (kDecLong - 1)) == 0) {
       // right after a refill (>= 33 window bits): one code decoded arithmetically --
       // near the segment end, or a code longer than 12 bits
       const uint32_t top = (uint32_t)(r.win >> 32);
@@ -1934,9 +1960,8 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       int32_t v = ((top >> sa) & 1u) ? (int32_t)m : -(int32_t)m;
       if (L <= 32u) {
         r.win <<= L;
-        r.nwin -= (int32_t)L;
       } else {  // a code longer than 32 bits (or a malformed one)
-        const uint64_t pos = b1 - (uint64_t)rem;
+        const uint64_t pos = b0 + (uint64_t)cons;
         const CodeVal cv = slow_code(base, cap, pos);
         if (cv.L == 0) {
           bad = 1;
@@ -1946,6 +1971,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
         d = cv.d;
         v = cv.v;
         r.init(base, cap, pos + L);
+        fill = cons + (int32_t)L + r.nwin;
       }
       // the run may come from far before the tile: bound it before scaling to bytes
       const int32_t rel_now = ((int32_t)(relb - my_addr)) >> 2;
@@ -1953,26 +1979,28 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       bad |= rel_new >= (uint32_t)kTE ? 1u : 0u;
       relb = my_addr + 4u * min(rel_new, (uint32_t)kTE - 1);
       acc_add_at<FACC>(relb, v, scale);
-      rem -= (int32_t)L;
+      cons += (int32_t)L;
     }
-    if (r.nwin <= 32) {
-      r.win |= (uint64_t)r.pop32() << (32 - r.nwin);
-      r.nwin += 32;
+    if (fill - cons <= 32) {
+      r.win |= (uint64_t)r.pop32() << (32 - (fill - cons));
+      fill += 32;
     }
   }
   // every decoded value must have landed inside this tile's accumulator
   bad |= (relb < lo_addr || relb >= hi_addr) ? 1u : 0u;
-  if (bad || rem != 0) atomicOr(err, 1);
+  if (bad || cons != total) atomicOr(err, 1);
 }
 
 // Persistent: each workgroup builds the decode table once, then walks tiles
 // (tiles_per_wg at a time) with one lane per client segment, accumulating the
 // clients' values in LDS and writing the tile's sum / dequantised values.
 template <bool FACC>
-__global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
-  extern __shared__ int32_t smem[];  // [kLutSize] table, then [tiles_per_wg][kTE] sums
-  uint32_t* lut = (uint32_t*)smem;
-  int32_t* acc = smem + kLutSize;
+#ifndef FC_DEC_WPE
+#define FC_DEC_WPE 5  // waves per SIMD the register budget is held to
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_DEC_WPE))) void k_decode(DecodeArgs a) {
+  __shared__ uint32_t lut[kLutSize];  // static: table reads fold its base into the offset
+  extern __shared__ int32_t acc[];     // [tiles_per_wg][kTE] sums
   const int tid = threadIdx.x;
   const int tiles_per_wg = kThreads / a.lanes_per_tile;
   for (int i = tid; i < kLutSize; i += kThreads) lut[i] = lut_entry((uint32_t)i);
@@ -2637,7 +2665,7 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   const bool facc = a.client_scale != nullptr;
   void (*kern)(DecodeArgs) = facc ? k_decode<true> : k_decode<false>;
   const int tpw = kThreads / lpt;
-  const size_t lds = (size_t)kLutSize * 4 + (size_t)tpw * kTE * sizeof(int32_t);
+  const size_t lds = (size_t)tpw * kTE * sizeof(int32_t);  // + the static kLutSize-word table
   int dev = 0, ncu = 256, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);

@@ -38,7 +38,8 @@ def main():
     with open(f) as fh:
       for row in csv.DictReader(fh):
         name = row["Kernel_Name"]
-        key = "k_encode" if "k_encode<" in name else ("k_decode" if "k_decode(" in name else None)
+        key = "k_encode" if "k_encode<" in name else (
+            "k_decode" if ("k_decode(" in name or "k_decode<" in name) else None)
         if key:
           per[key][row["Counter_Name"]].append(float(row["Counter_Value"]))
   out = {}
