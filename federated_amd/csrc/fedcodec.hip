@@ -51,7 +51,7 @@ constexpr uint32_t kNoPos = 0x1FFF; // "no nonzero" in a 13-bit tile-relative fi
 // one 64-B line each; stream k hands out tickets k, k + K, k + 2K, ... in order.
 constexpr int kTicketShards = 32;
 #ifndef FC_LOOKBACK_WIN
-#define FC_LOOKBACK_WIN 64
+#define FC_LOOKBACK_WIN 0  // 0: chosen per launch from the tiles in flight per client
 #endif
 constexpr int kLookbackWin = FC_LOOKBACK_WIN;  // statuses prefetched for the vector look-back
 constexpr int kShardStride = 16;  // uint32 words between counters (64 B)
@@ -295,6 +295,7 @@ struct EncodeArgs {
   int32_t* slow_list;    // [nclients]
   uint32_t* counter2;    // exact kernel's ticket counter
   uint32_t div_m, div_l;  // ticket / nclients by multiply-high (Granlund-Montgomery)
+  int32_t lb_lane0;       // first lane whose status the look-back prefetches (64 - window)
 };
 
 __device__ __forceinline__ uint32_t div_clients(const EncodeArgs& a, uint32_t n) {
@@ -469,14 +470,130 @@ __device__ unsigned long long g_stamps[16];
 #else
 #define FC_COUNT(i, v) do {} while (0)
 #endif
+// Multi-window vector look-back, for when the 64 tiles before t hold no
+// inclusive prefix (few clients: many tiles of one client in flight).  Lane i
+// holds tile wbase+i of the current 64-tile window.  A window of 64 aggregates
+// is folded with the same DPP scans as lookback_vec into a segment of its own
+// and the walk moves 64 tiles back, until a window holds a prefix.  A window's
+// tail is its newest tile's tail whenever that tile's body has >= 32 bits;
+// otherwise the scalar lookback() does the whole fold (rare: a nearly empty
+// tile).  Out of line: it keeps its registers off the common path.
+constexpr uint32_t kSegSlow = 0xFFFFFFFFu;  // lookback_deep's "a slow tile" result (has_nz)
+__device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, int lane,
+                                          uint32_t* spin_err, uint64_t pre1, uint64_t pre2) {
+  // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
+  // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
+  Seg S = seg_identity();  // fold of the newer windows already walked
+  int32_t wbase = t - 64;
+  uint32_t h1 = (uint32_t)(pre1 >> 32), l1 = (uint32_t)pre1, h2 = (uint32_t)(pre2 >> 32), l2 = (uint32_t)pre2;
+  for (;;) {
+    const int32_t ti = wbase + lane;
+    if (ti < 0) {
+      h1 = h2 = 0x80000000u;
+      l1 = l2 = 0u;
+    }
+    // a status is readable once both granules carry the same nonzero flag
+    bool valid = h1 >= 0x40000000u && (h1 ^ h2) < 0x40000000u;
+    uint32_t spins = 0;
+    uint64_t pre;
+    for (;;) {
+      pre = __ballot(valid && h1 >= 0x80000000u);  // inclusive prefix (or slow)
+      const uint64_t val = __ballot(valid);
+      const uint64_t need = pre ? ~0ull << (63 - (int)__clzll(pre)) : ~0ull;
+      if ((val & need) == need) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) {
+        if (lane == 0) atomicOr(spin_err, 1u);
+        Seg r = seg_identity();
+        r.has_nz = 1;
+        r.first = r.last = -1;
+        return r;
+      }
+      if (!valid) {
+        const uint64_t w1 = ld_agent(status_c + 2 * (int64_t)ti);
+        const uint64_t w2 = ld_agent(status_c + 2 * (int64_t)ti + 1);
+        h1 = (uint32_t)(w1 >> 32);
+        l1 = (uint32_t)w1;
+        h2 = (uint32_t)(w2 >> 32);
+        l2 = (uint32_t)w2;
+        valid = h1 >= 0x40000000u && (h1 ^ h2) < 0x40000000u;
+      }
+    }
+    const int p = pre ? 63 - (int)__clzll(pre) : -1;  // nearest (newest) prefix, -1: none in this window
+    uint32_t ph = 0;
+    if (p >= 0) {
+      ph = __builtin_amdgcn_readlane(h1, p);
+      if (ph >= 0xC0000000u) {  // a slow tile: give up
+        Seg r = seg_identity();
+        r.has_nz = kSegSlow;
+        return r;
+      }
+    }
+    Seg r;
+    r.has_nz = 1;
+    r.first = -1;
+    // prefix at lane p: [61:36] last + 1, [35:0] bits
+    const int32_t plast = (int32_t)((ph >> 4) & ((1u << 26) - 1)) - 1;
+    const uint64_t pbody = p >= 0 ? ((uint64_t)(ph & 0xFu) << 32) | __builtin_amdgcn_readlane(l1, p) : 0ull;
+    if (p == 63) {  // the newest tile's own inclusive prefix
+      r.last = plast;
+      r.body = pbody;
+      r.tail = __builtin_amdgcn_readlane(l2, 63);
+      return seg_combine(r, S);
+    }
+    // aggregates above the prefix: [61:49] first_rel, [48:36] last_rel, body < 2^32
+    const bool agg = lane > p;
+    const uint32_t fr = (h1 >> 17) & 0x1FFFu, lr = (h1 >> 4) & 0x1FFFu;
+    const bool nz = agg && fr != kNoPos;
+    const int32_t tb = ti * kTE;
+    int32_t lastv = agg ? -1 : (lane == p ? plast : -1);
+    lastv = nz ? tb + (int32_t)lr : lastv;
+    const int32_t M = dpp_incl_max(lastv);
+    const int32_t Mx = dpp_shr1(M, -1);  // last nonzero before this tile (-1: none in the window)
+    uint32_t contrib = agg ? l1 : 0u;
+    // no prefix: the window's first nonzero has no run code yet (seg_combine adds it)
+    if (nz && (p >= 0 || Mx >= 0)) contrib += glen((uint32_t)(tb + (int32_t)fr - Mx));
+    const uint32_t csum = (uint32_t)wave_sum_i((int32_t)contrib);
+    if (__builtin_amdgcn_readlane(l1, 63) < 32u) {  // short newest body: exact scalar fold
+      bool slow = false;
+      Seg r2 = lookback(status_c, t, lane, spin_err, slow);
+      if (slow) r2.has_nz = kSegSlow;
+      return r2;
+    }
+    r.tail = __builtin_amdgcn_readlane(l2, 63);  // the newest body holds the last 32 bits
+    r.body = pbody + csum;
+    if (p >= 0) {
+      r.last = lane63(M);
+      return seg_combine(r, S);
+    }
+    // 64 aggregates and no prefix: fold them into a segment, walk 64 tiles back
+    const uint64_t nzm = __ballot(nz);
+    r.has_nz = nzm != 0;
+    r.first = nzm ? __builtin_amdgcn_readlane(tb + (int32_t)fr, (int)__builtin_ctzll(nzm)) : 0;
+    r.last = lane63(M);
+    if (r.has_nz) S = seg_combine(r, S);
+    wbase -= 64;
+    const int32_t tn = wbase + lane;
+    h1 = h2 = l1 = l2 = 0u;  // unreadable until loaded (ti < 0: root, set above)
+    if (tn >= 0) {
+      const uint64_t w1 = ld_agent(status_c + 2 * (int64_t)tn);
+      const uint64_t w2 = ld_agent(status_c + 2 * (int64_t)tn + 1);
+      h1 = (uint32_t)(w1 >> 32);
+      l1 = (uint32_t)w1;
+      h2 = (uint32_t)(w2 >> 32);
+      l2 = (uint32_t)w2;
+    }
+  }
+}
+
 // Vectorised look-back (the encoder's common case).  Lane i holds tile
 // t-64+i (lane 63 = t-1); pre1/pre2 are those statuses, loaded earlier.  Once
 // the nearest inclusive prefix p and every aggregate after it are visible, the
 // fold is two DPP scans instead of a serial scalar walk: the last nonzero
 // before each aggregate (max-scan of the aggregates' last positions), its
 // first run code length, and the sum of bodies.  The combined tail is the
-// newest tile's tail whenever that tile's body has >= 32 bits; otherwise (and
-// when no prefix is within 64 tiles) the scalar lookback() does the fold.
+// newest tile's tail whenever that tile's body has >= 32 bits; otherwise the
+// scalar lookback() does the fold.  No prefix within 64 tiles: lookback_deep().
 __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t, int lane,
                                             uint32_t* spin_err, bool& slow, uint64_t pre1,
                                             uint64_t pre2) {
@@ -495,9 +612,14 @@ __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t,
   for (;;) {
     const uint64_t pre = __ballot(valid && h1 >= 0x80000000u);  // inclusive prefix (or slow)
     const uint64_t val = __ballot(valid);
-    if (pre == 0) {  // no prefix in the window: scalar walk
+    if (pre == 0) {  // no prefix in the window: walk 64-tile windows
       FC_COUNT(10, 1);
-      return lookback(status_c, t, lane, spin_err, slow);
+      Seg r = lookback_deep(status_c, t, lane, spin_err, pre1, pre2);
+      if (r.has_nz == kSegSlow) {
+        slow = true;
+        r = seg_identity();
+      }
+      return r;
     }
     p = 63 - (int)__clzll(pre);  // nearest (newest) prefix
     const uint64_t need = ~0ull << p;
@@ -1162,10 +1284,11 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
     // the pending tile's look-back window (lane i: tile pt-64+i), fetched now and
     // used after this tile's work
     uint64_t pw1 = 0, pw2 = 0;  // not fetched: unreadable (lookback_vec re-polls it if needed)
-    // only the kLookbackWin nearest statuses are fetched: with C clients and W waves
-    // about W / C tiles of a client are in flight, so the nearest inclusive prefix is
-    // rarely further back (lookback_vec falls back to the scalar walk when it is)
-    if (!(FC_ABL & 16) && pv && pt + lane >= 64 && lane >= 64 - kLookbackWin) {
+    // only the nearest statuses are fetched (window chosen per launch): every fetched
+    // status is a coherent read, so with few clients -- many tiles of one client in
+    // flight -- a short window is cheaper even when the nearest inclusive prefix
+    // lies beyond it (lookback_vec then polls further back itself)
+    if (!(FC_ABL & 16) && pv && pt + lane >= 64 && lane >= a.lb_lane0) {
       const uint64_t* sp = a.status + 2 * ((int64_t)pc * a.T + pt - 64 + lane);
       pw1 = ld_agent(sp);
       pw2 = ld_agent(sp + 1);
@@ -2625,15 +2748,22 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   }
   if ((uint64_t)nclients * (uint64_t)T >= (1ull << 32)) return fail(-1, "too many tiles (nclients x tiles >= 2^32)");
   // Persistent grid no larger than what is co-resident (every ticket stream has a
-  // running workgroup); few clients: cap the tiles in flight per client so the
-  // look-back windows stay short.
+  // running workgroup); very few clients: cap the tiles in flight per client (about
+  // 256) so a look-back walks at most a few 64-tile windows.
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kEncThreads, 0) != hipSuccess || per_cu < 1)
     per_cu = 1;
-  int64_t max_grid = std::min<int64_t>((int64_t)ncu * per_cu, std::max<int64_t>(128, 64LL * nclients));
+  int64_t max_grid = std::min<int64_t>((int64_t)ncu * per_cu, std::max<int64_t>(128, 128LL * nclients));
   if (const char* g = getenv("FEDCODEC_ENC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
   const int grid = (int)std::min<int64_t>(total, max_grid);
   a.nshards = (uint32_t)std::min(kTicketShards, grid);
+  {  // look-back prefetch window: 64 statuses when few tiles of a client are in flight,
+     // 16 when many are (measured at 25 M: C = 128 -13 %, C = 1024 +2 % with 16)
+    int win = kLookbackWin;
+    if (win <= 0) win = 2 * (int64_t)grid / nclients <= 24 ? 64 : 16;
+    if (const char* w = getenv("FEDCODEC_LB_WIN")) win = atoi(w);  // test knob
+    a.lb_lane0 = 64 - std::max(1, std::min(64, win));
+  }
   hipLaunchKernelGGL(k_client_params, dim3((nclients + 255) / 256), dim3(256), 0, s, a,
                      (ClientParam*)a.cparams, (int)(!int_in && mode != FC_UNIFORM));
   if (hipGetLastError() != hipSuccess) return fail(-10, "k_client_params launch");

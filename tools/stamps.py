@@ -22,8 +22,9 @@ if HAVE:
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev)
 g.manual_seed(1)
-pool = [torch.randn(P, generator=g, device=dev) for _ in range(4)]
-rows = [pool[c % 4] for c in range(C)]
+NPOOL = int(os.environ.get("POOL", 4)) or C  # POOL=0: a distinct delta per client
+pool = [torch.randn(P, generator=g, device=dev) for _ in range(NPOOL)]
+rows = [pool[c % NPOOL] for c in range(C)]
 ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
 seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
 batch = codec.EncodedBatch(P, C, [P + 1024] * C, dev)
