@@ -149,12 +149,19 @@ def test_reference_known_answers(gpu):
     assert int(b.bits()[0]) == nbits
 
 
-@pytest.mark.parametrize("grid", ["1", "5", "64"])
-def test_encode_many_tiles_per_workgroup(gpu, grid, monkeypatch):
-  """Persistent workgroups that each take many tiles (LDS window reuse) and a
-  look-back that crosses many tiles (grid 64 over 2 x 245 tiles)."""
-  monkeypatch.setenv("FEDCODEC_ENC_GRID", grid)
-  rng = np.random.default_rng(int(grid))
+@pytest.mark.parametrize("grid,win", [("1", None), ("5", None), ("64", None), ("512", None),
+                                      ("default", None), ("512", "4"), ("4096", "64")])
+def test_encode_many_tiles_per_workgroup(gpu, grid, win, monkeypatch):
+  """Persistent workgroups that each take many tiles (LDS window reuse) and
+  look-backs that cross many tiles: with 2 clients x 977 tiles and hundreds of
+  waves, the nearest inclusive prefix often lies beyond 64 tiles, so the
+  multi-window walk (lookback_deep) runs, with short (4) and full (64)
+  prefetch windows."""
+  if grid != "default":
+    monkeypatch.setenv("FEDCODEC_ENC_GRID", grid)
+  if win is not None:
+    monkeypatch.setenv("FEDCODEC_LB_WIN", win)
+  rng = np.random.default_rng(len(grid) * 7 + (int(win) if win else 0))
   P, C = 1_000_003, 2
   xs = [(rng.standard_normal(P) * 0.7).astype(np.float32) for _ in range(C)]
   xs[1][100_000:900_000] = 0.0  # long zero runs crossing many tiles
