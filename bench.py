@@ -53,6 +53,10 @@ def parse():
   ap.add_argument("--cap-bytes-per-elem", type=float, default=1.0)
   ap.add_argument("--no-cpu-baseline", action="store_true")
   ap.add_argument("--cpu-sample-clients", type=int, default=32)
+  ap.add_argument("--dump-result", default="",
+                  help="rank 0 saves the round's dequantised sum (.npy) to compare world sizes")
+  ap.add_argument("--slabs", type=int, default=4,
+                  help="N > 1: tile ranges decoded in turn, each all-reduced while the next decodes")
   return ap.parse_args()
 
 
@@ -62,8 +66,16 @@ def setup_dist(args):
   local = int(os.environ.get("LOCAL_RANK", "0"))
   if world > 1:
     import torch.distributed as dist  # pylint: disable=g-import-not-at-top
+    # rehearsal knobs for a 1-GPU box (never set by the driver): every rank on one
+    # device, gloo instead of RCCL
+    backend = os.environ.get("FEDCODEC_BENCH_BACKEND", "nccl")
+    if os.environ.get("FEDCODEC_BENCH_ONE_DEVICE"):
+      local = 0
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if backend == "nccl":
+      dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+      dist.init_process_group(backend)
   else:
     torch.cuda.set_device(0)
   return rank, world
@@ -143,7 +155,9 @@ def main():
   g.manual_seed(20251015 + rank)
   npool = args.pool if args.pool > 0 else Cg
   pool = []
-  for _ in range(npool):
+  for i in range(npool):
+    if npool == Cg:  # a delta per client, seeded by its global index: any --gpus N sums the same round
+      g.manual_seed(20251015 + rank * Cg + i)
     t = torch.randn(P, generator=g, device=dev, dtype=torch.float32)
     pool.append(t.mul_(args.sigma))
   rows = [pool[c % npool] for c in range(Cg)]
@@ -159,6 +173,10 @@ def main():
   if world > 1:
     import torch.distributed as dist  # pylint: disable=g-import-not-at-top
 
+  T = codec.num_tiles(P)
+  nslab = max(1, min(args.slabs, T))
+  bounds = [T * k // nslab for k in range(nslab + 1)]
+
   def step():
     codec.quantize_encode(None, args.step_size, seeds, mode, ptrs=ptrs, P=P, out=batch,
                           stream=stream)
@@ -166,8 +184,17 @@ def main():
       codec.decode_accumulate(batch, want_sum=False, out=out, step=args.step_size, err=err,
                               stream=stream)
     else:
-      codec.decode_accumulate(batch, sum_out=isum, err=err, stream=stream)
-      dist.all_reduce(isum)
+      # decode tile range k, then all-reduce it (RCCL on its own stream, ordered after
+      # the decode) while range k+1 decodes; the int32 sum is exact in any order
+      err.zero_()
+      works = []
+      for k in range(nslab):
+        codec.decode_accumulate(batch, sum_out=isum, err=err, stream=stream,
+                                tiles=(bounds[k], bounds[k + 1]))
+        lo, hi = bounds[k] * 1024, min(P, bounds[k + 1] * 1024)
+        works.append(dist.all_reduce(isum[lo:hi], async_op=True))
+      for w in works:
+        w.wait()
       _lib.call("fc_dequantize", _lib.ptr(isum), P, float(args.step_size), None, _lib.ptr(out),
                 _lib.stream_handle(stream))
 
@@ -196,6 +223,8 @@ def main():
     dist.barrier()
   wall = time.perf_counter() - t0
   t_dev = ev0.elapsed_time(ev1) / 1e3
+  if args.dump_result and rank == 0:
+    np.save(args.dump_result, out.cpu().numpy())
   t = torch.tensor([max(wall, t_dev)], dtype=torch.float64, device=dev)
   if world > 1:
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -165,9 +165,11 @@ def rlgamma_encode(qs, caps=None):
 
 
 def decode_accumulate(batch, sum_in=None, want_sum=True, out=None, step=1.0, noise_sum=None,
-                      stream=None, err=None, sum_out=None):
+                      stream=None, err=None, sum_out=None, tiles=None):
   """Decode every client's code and sum over clients (int32, wrapping).
 
+  tiles=(begin, end): only tiles [begin, end) of 1024 elements are decoded and
+  written (fc_decode_accumulate_tiles; err is OR'ed into, not cleared).
   Returns (sum_out or None, out or None, err tensor).
   """
   _lib.require_gpu()
@@ -176,10 +178,16 @@ def decode_accumulate(batch, sum_in=None, want_sum=True, out=None, step=1.0, noi
     sum_out = torch.empty(batch.P, dtype=torch.int32, device=device)
   if err is None:
     err = torch.zeros(1, dtype=torch.int32, device=device)
-  _lib.call("fc_decode_accumulate", _lib.ptr(batch.stream), _lib.ptr(batch.stream_off),
-            _lib.ptr(batch.stream_cap), _lib.ptr(batch.idx), batch.nclients, batch.P,
-            _lib.ptr(sum_in), _lib.ptr(sum_out if want_sum else None), _lib.ptr(out),
-            float(step), _lib.ptr(noise_sum), _lib.ptr(err), _lib.stream_handle(stream))
+  if tiles is None:
+    _lib.call("fc_decode_accumulate", _lib.ptr(batch.stream), _lib.ptr(batch.stream_off),
+              _lib.ptr(batch.stream_cap), _lib.ptr(batch.idx), batch.nclients, batch.P,
+              _lib.ptr(sum_in), _lib.ptr(sum_out if want_sum else None), _lib.ptr(out),
+              float(step), _lib.ptr(noise_sum), _lib.ptr(err), _lib.stream_handle(stream))
+  else:
+    _lib.call("fc_decode_accumulate_tiles", _lib.ptr(batch.stream), _lib.ptr(batch.stream_off),
+              _lib.ptr(batch.stream_cap), _lib.ptr(batch.idx), batch.nclients, batch.P,
+              int(tiles[0]), int(tiles[1]), _lib.ptr(sum_in), _lib.ptr(sum_out if want_sum else None),
+              _lib.ptr(out), float(step), _lib.ptr(noise_sum), _lib.ptr(err), _lib.stream_handle(stream))
   return (sum_out if want_sum else None), out, err
 
 

@@ -1715,6 +1715,7 @@ struct DecodeArgs {
   int32_t* err;
   const float* client_scale;  // FACC: per-client dequantisation step
   const float* fsum_in;       // FACC: optional float partial sum to add
+  int32_t t_begin, t_end;     // tiles decoded: [t_begin, t_end)
 };
 
 // MSB-first bit reader over one client's code: a 64-bit window plus one
@@ -2130,13 +2131,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_DEC
   const int sub = tid / a.lanes_per_tile;
   const int l = tid - sub * a.lanes_per_tile;
   const uint32_t my_addr = (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * kTE);
-  const int64_t ngroups = (a.T + tiles_per_wg - 1) / tiles_per_wg;
+  const int64_t ngroups = (a.t_end - a.t_begin + tiles_per_wg - 1) / tiles_per_wg;
+  const int64_t e_end = min(a.P, (int64_t)a.t_end * kTE);  // elements this launch writes
   for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const int64_t t0 = grp * tiles_per_wg;
+    const int64_t t0 = a.t_begin + grp * tiles_per_wg;
     for (int i = tid; i < tiles_per_wg * kTE; i += kThreads) acc[i] = 0;
     __syncthreads();
     const int64_t t = t0 + sub;
-    if (t < a.T) {
+    if (t < a.t_end) {
       const int64_t tile_base = t * kTE;
       for (int c = l; c < a.nclients; c += a.lanes_per_tile) {
         const int64_t ib = (int64_t)c * (a.T + 1) + t;
@@ -2151,7 +2153,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_DEC
     __syncthreads();
     for (int i = tid; i < tiles_per_wg * kTE; i += kThreads) {
       const int64_t e = t0 * kTE + i;
-      if (e >= a.P) break;
+      if (e >= e_end) break;
       if (FACC) {  // float32 sum of dequantised clients (+ a float partial sum)
         float f = __int_as_float(acc[i]);
         if (a.fsum_in) f = a.fsum_in[e] + f;
@@ -2777,7 +2779,8 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
 
 // Shared launcher of k_decode (int32 client sum, or float sum of scaled clients).
 int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap,
-                  const uint64_t* idx, int32_t nclients, int64_t P, int32_t* err, void* stream) {
+                  const uint64_t* idx, int32_t nclients, int64_t P, int32_t* err, void* stream,
+                  int64_t tile_begin = 0, int64_t tile_end = -1, bool reset_err = true) {
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
   if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
   if (!stream_buf || !stream_off || !stream_cap || !idx || !err) return fail(-1, "null required pointer");
@@ -2789,6 +2792,10 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   a.P = P;
   a.T = (int32_t)tiles_for(P);
   a.err = err;
+  if (tile_end < 0) tile_end = a.T;
+  if (tile_begin < 0 || tile_begin >= tile_end || tile_end > a.T) return fail(-1, "tile range must satisfy 0 <= begin < end <= tiles");
+  a.t_begin = (int32_t)tile_begin;
+  a.t_end = (int32_t)tile_end;
   int lpt = 256;
   while (lpt > 64 && lpt / 2 >= nclients) lpt /= 2;
   a.lanes_per_tile = lpt;
@@ -2801,13 +2808,13 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
-  const int64_t ngroups = (a.T + tpw - 1) / tpw;
+  const int64_t ngroups = (a.t_end - a.t_begin + tpw - 1) / tpw;
   // 5 workgroups/CU: more waves only add L2 line thrash (measured 4.2 ms at 5/CU vs 5.0 at 7/CU)
   int64_t max_grid = (int64_t)ncu * std::min(per_cu, 5);
   if (const char* g = getenv("FEDCODEC_DEC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
   const dim3 grid((unsigned)std::min<int64_t>(ngroups, max_grid));
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(err, 0, sizeof(int32_t), s) != hipSuccess) return fail(-10, "memset err");
+  if (reset_err && hipMemsetAsync(err, 0, sizeof(int32_t), s) != hipSuccess) return fail(-10, "memset err");
   hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, s, a);
   return check_launch("k_decode");
 }
@@ -2881,6 +2888,21 @@ int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off, c
   a.step = step;
   a.noise_sum = noise_sum;
   return decode_common(a, stream_buf, stream_off, stream_cap, idx, nclients, P, err, stream);
+}
+
+int fc_decode_accumulate_tiles(const uint8_t* stream_buf, const int64_t* stream_off,
+                               const int64_t* stream_cap, const uint64_t* idx, int32_t nclients, int64_t P,
+                               int32_t tile_begin, int32_t tile_end, const int32_t* sum_in, int32_t* sum_out,
+                               float* out, float step, const float* noise_sum, int32_t* err, void* stream) {
+  if (!sum_out && !out) return fail(-1, "one of sum_out / out required");
+  DecodeArgs a{};
+  a.sum_in = sum_in;
+  a.sum_out = sum_out;
+  a.out = out;
+  a.step = step;
+  a.noise_sum = noise_sum;
+  return decode_common(a, stream_buf, stream_off, stream_cap, idx, nclients, P, err, stream, tile_begin,
+                       tile_end, false);
 }
 
 int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream_off,

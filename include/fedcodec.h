@@ -129,6 +129,17 @@ int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off,
                          int64_t P, const int32_t* sum_in, int32_t* sum_out, float* out,
                          float step, const float* noise_sum, int32_t* err, void* stream);
 
+/* fc_decode_accumulate restricted to tiles [tile_begin, tile_end) of 1024
+ * elements: only elements [1024 * tile_begin, min(P, 1024 * tile_end)) of
+ * sum_out / out are written.  err is OR'ed into, not cleared (zero it before the
+ * first range).  Lets a multi-GPU round all-reduce finished tile ranges while
+ * later ranges decode (same accumulate/merge as fc_decode_accumulate). */
+int fc_decode_accumulate_tiles(const uint8_t* stream_buf, const int64_t* stream_off,
+                               const int64_t* stream_cap, const uint64_t* idx, int32_t nclients,
+                               int64_t P, int32_t tile_begin, int32_t tile_end,
+                               const int32_t* sum_in, int32_t* sum_out, float* out, float step,
+                               const float* noise_sum, int32_t* err, void* stream);
+
 /* QSGD server side: out[i] = [fsum_in[i] +] sum over clients of
  * float(q_c[i]) * client_scale[c] in float32 (summation order unspecified: the
  * reference's client-order float sum is matched within a tolerance). */

@@ -51,6 +51,11 @@ def test_argument_validation_without_gpu():
   rc = lib.fc_decode_accumulate(None, None, None, None, 1, (1 << 26), None, None, None, 1.0, None,
                                 None, None)
   assert rc != 0
+  dummy = ctypes.c_int64(0)
+  p = ctypes.addressof(dummy)
+  for tb, te in ((0, 0), (1, 1), (-1, 2), (0, 99)):  # P = 5000: 5 tiles
+    rc = lib.fc_decode_accumulate_tiles(p, p, p, p, 1, 5000, tb, te, None, p, None, 1.0, None, p, None)
+    assert rc != 0 and b"tile range" in lib.fc_last_error()
 
 
 def test_product_package_never_imports_the_oracle():

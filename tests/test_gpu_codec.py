@@ -178,3 +178,28 @@ def test_encode_many_tiles_per_workgroup(gpu, grid, win, monkeypatch):
   s, _, err = codec.decode_accumulate(batch)
   assert int(err.item()) == 0
   np.testing.assert_array_equal(s.cpu().numpy(), acc.astype(np.int32))
+
+
+def test_decode_tile_ranges_match_full_decode(gpu):
+  """fc_decode_accumulate_tiles over consecutive tile ranges writes exactly the
+  full decode (the multi-GPU path all-reduces finished ranges while later ones
+  decode); a range never touches elements outside it."""
+  rng = np.random.default_rng(11)
+  P, C = 10_000, 3  # 10 tiles, the last partial
+  xs = [(rng.standard_normal(P) * 1.3).astype(np.float32) for _ in range(C)]
+  seeds = np.array([[1, 2], [3, 4], [5, 6]], np.int64)
+  batch = codec.quantize_encode_checked([torch.from_numpy(x).to(gpu) for x in xs], 0.5,
+                                        torch.from_numpy(seeds), _lib.STOCHASTIC)
+  full, fout, err = codec.decode_accumulate(batch, out=torch.empty(P, device=gpu), step=0.5)
+  assert int(err.item()) == 0
+  part = torch.full((P,), 12345, dtype=torch.int32, device=gpu)
+  pout = torch.full((P,), -7.0, dtype=torch.float32, device=gpu)
+  err = torch.zeros(1, dtype=torch.int32, device=gpu)
+  for tb, te in ((0, 3), (3, 4), (4, 10)):
+    codec.decode_accumulate(batch, sum_out=part, out=pout, step=0.5, err=err, tiles=(tb, te))
+    hi = min(P, te * 1024)
+    np.testing.assert_array_equal(part[:hi].cpu().numpy(), full[:hi].cpu().numpy())
+    assert (part[hi:].cpu().numpy() == 12345).all()
+    assert (pout[hi:].cpu().numpy() == -7.0).all()
+  np.testing.assert_array_equal(pout.cpu().numpy(), fout.cpu().numpy())
+  assert int(err.item()) == 0
