@@ -30,17 +30,34 @@ def allreduce_sum_(t, group=None):
   return t
 
 
-def aggregate_round(local_rows, step, local_seeds, mode, group=None, prescale=None):
+def aggregate_round(local_rows, step, local_seeds, mode, group=None, prescale=None, slabs=4):
   """Encode + decode this rank's clients, all-reduce the int32 sums, dequantise.
 
+  The decode runs in `slabs` tile ranges (fc_decode_accumulate_tiles); each
+  range's sum is all-reduced asynchronously (the collective's stream waits for
+  that range's decode) while the next range decodes.  Integer sums make the
+  result independent of the range split and of the ring order.
   Returns (float32 result [P], local EncodedBatch).  Dithered mode also
   all-reduces the float32 noise sum (tolerance, as TFF's federated_sum).
   """
   batch = codec.quantize_encode_checked(local_rows, step, local_seeds, mode, prescale=prescale)
-  isum, _, err = codec.decode_accumulate(batch, want_sum=True)
+  P = batch.P
+  isum = torch.empty(P, dtype=torch.int32, device=batch.device)
+  err = torch.zeros(1, dtype=torch.int32, device=batch.device)
+  multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+  T = codec.num_tiles(P)
+  n = max(1, min(int(slabs), T)) if multi else 1
+  bounds = [T * k // n for k in range(n + 1)]
+  works = []
+  for k in range(n):
+    codec.decode_accumulate(batch, sum_out=isum, err=err, tiles=(bounds[k], bounds[k + 1]))
+    if multi:
+      lo, hi = bounds[k] * 1024, min(P, bounds[k + 1] * 1024)
+      works.append(dist.all_reduce(isum[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True))
+  for w in works:
+    w.wait()
   if int(err.item()):
     raise RuntimeError("malformed run-length gamma code")
-  allreduce_sum_(isum, group)
   noise = None
   if mode == _lib.DITHERED:
     noise = codec.noise_sum(local_seeds, batch.P, isum.device)
