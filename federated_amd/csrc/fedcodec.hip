@@ -838,8 +838,10 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
   if (__ballot(big) == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint32_t qi = (uint32_t)(int32_t)q[k];
-      const uint32_t e = clut[(dv[k] << 6) | (qi & 63u)];  // zero -> empty code
+      // byte offset 4 * ((dv << 6) | (q & 63)): q * 4 + 1.5 * 2^23 is exact for |q| <= 31
+      // and its low 8 bits are 4q mod 256 -- one FMA instead of a float->int conversion
+      const uint32_t qb = __float_as_uint(fmaf(q[k], 4.0f, 12582912.0f)) & 0xFCu;
+      const uint32_t e = *(const uint32_t*)((const char*)clut + ((dv[k] << 8) | qb));  // zero -> empty code
       const uint32_t L = e >> 16;
       r.acc = k == 0 ? (uint64_t)(e & 0xFFFFu) : ((r.acc << L) | (e & 0xFFFFu));
       r.len += L;
