@@ -1720,118 +1720,6 @@ struct DecodeArgs {
   int32_t t_begin, t_end;     // tiles decoded: [t_begin, t_end)
 };
 
-// MSB-first bit reader over one client's code: a 64-bit window plus one
-// prefetched 32-bit word, so each refill's load is issued ~one refill early.
-struct BitReader {
-  const uint4* p;    // next 16-byte block to fetch
-  const uint4* end;  // first block beyond the client's region
-  uint4 nxt;         // prefetched raw block, consumed one reservoir later
-  uint32_t nxtok;    // nxt lies inside the region
-  uint64_t rhi, rlo; // reservoir: next 128 bits after the window, MSB aligned
-  int rbits;         // valid bits in the reservoir (multiple of 32)
-  uint64_t win;      // next bits, MSB aligned
-  int nwin;          // valid bits in win (>= 32 after refill)
-
-  __device__ __forceinline__ void prefetch() {
-    nxtok = p < end;
-    nxt = *(nxtok ? p : end - 1);  // unconditional 16-byte load: no branch, no early wait
-    ++p;
-  }
-  __device__ __forceinline__ void load_reservoir() {
-    const uint4 b = nxtok ? nxt : make_uint4(0, 0, 0, 0);
-    rhi = ((uint64_t)bswap32(b.x) << 32) | bswap32(b.y);
-    rlo = ((uint64_t)bswap32(b.z) << 32) | bswap32(b.w);
-    rbits = 128;
-    prefetch();
-  }
-  __device__ __forceinline__ uint32_t next_word() {
-    if (rbits == 0) load_reservoir();
-    const uint32_t w = (uint32_t)(rhi >> 32);
-    rhi = (rhi << 32) | (rlo >> 32);
-    rlo <<= 32;
-    rbits -= 32;
-    return w;
-  }
-  __device__ __forceinline__ void init(const uint8_t* base, int64_t cap, uint64_t bit) {
-    p = (const uint4*)base + (bit >> 7);
-    end = (const uint4*)base + (cap >> 4);
-    prefetch();
-    load_reservoir();
-    for (int i = (int)((bit >> 5) & 3); i > 0; --i) (void)next_word();
-    win = ((uint64_t)next_word() << 32);
-    win |= next_word();
-    const int skip = (int)(bit & 31);
-    win <<= skip;
-    nwin = 64 - skip;
-  }
-  __device__ __forceinline__ void refill() {
-    if (nwin <= 32) {
-      win |= (uint64_t)next_word() << (32 - nwin);
-      nwin += 32;
-    }
-  }
-  // Consume n <= 32 bits (caller guarantees nwin >= n).
-  __device__ __forceinline__ uint32_t take(int n) {
-    const uint32_t v = (uint32_t)(win >> (64 - n));
-    win = n >= 64 ? 0 : win << n;
-    nwin -= n;
-    refill();
-    return v;
-  }
-  // Gamma-coded value (1 .. 2^32-1), general path.  Returns 0 on a malformed code.
-  __device__ __forceinline__ uint32_t gamma() {
-    int zeros = 0;
-    for (;;) {
-      int zz = win ? (int)__clzll(win) : 64;
-      if (zz >= nwin) {  // the whole window is zeros
-        zeros += nwin;
-        win = 0;
-        nwin = 0;
-        refill();
-        if (zeros > 31) return 0;
-        continue;
-      }
-      zeros += zz;
-      win <<= zz;
-      nwin -= zz;
-      refill();
-      break;
-    }
-    if (zeros > 31) return 0;
-    return take(zeros + 1);
-  }
-};
-
-__device__ __forceinline__ uint64_t shl64(uint64_t x, uint32_t n) { return n >= 64 ? 0 : x << n; }
-
-// One nonzero's code: run gamma d, sign bit, magnitude gamma m.  Returns the
-// bits consumed (0 on a malformed code).
-__device__ __forceinline__ uint32_t decode_code(BitReader& br, uint32_t& d, int32_t& val) {
-  const uint64_t w = br.win;
-  const uint32_t z1 = w ? (uint32_t)__clzll(w) : 64u;
-  const uint32_t L1 = 2u * z1 + 1u;
-  const uint64_t w3 = shl64(w, L1 + 1u);
-  const uint32_t z2 = w3 ? (uint32_t)__clzll(w3) : 64u;
-  const uint32_t L2 = 2u * z2 + 1u;
-  const uint32_t L = L1 + 1u + L2;
-  if (L <= (uint32_t)br.nwin && L1 <= 32u && L2 <= 32u) {  // fast path: whole code in the window
-    d = (uint32_t)(w >> (64u - L1));
-    const uint32_t s = (uint32_t)(shl64(w, L1) >> 63);
-    const uint32_t m = (uint32_t)(w3 >> (64u - L2));
-    val = (int32_t)(s ? m : 0u - m);
-    br.win = shl64(w3, L2);
-    br.nwin -= (int)L;
-    br.refill();
-    return L;
-  }
-  d = br.gamma();
-  const uint32_t s = br.take(1);
-  const uint32_t m = br.gamma();
-  val = (int32_t)(s ? m : 0u - m);
-  if (d == 0 || m == 0) return 0;
-  return 2u * (31u - __clz(d)) + 1u + 1u + 2u * (31u - __clz(m)) + 1u;
-}
-
 // General decode of one code at absolute bit position pos straight from
 // memory (any length; the rare path, kept out of line).  slow_code returns the
 // bits consumed, 0 on a malformed code.
