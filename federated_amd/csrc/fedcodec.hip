@@ -298,6 +298,17 @@ struct EncodeArgs {
   int32_t lb_lane0;       // first lane whose status the look-back prefetches (64 - window)
 };
 
+// The launch's EncodeArgs re-read from the kernarg segment (k_encode and
+// k_encode_exact take EncodeArgs as their only argument, at offset 0).  The
+// opaque asm makes every use a fresh scalar load, so fields needed only on rare
+// paths (slow tiles, overflow, spin errors, a client's last tile) do not hold
+// SGPRs for the whole persistent loop.
+__device__ __forceinline__ const EncodeArgs& enc_args_fresh() {
+  const EncodeArgs* p = (const EncodeArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *p;
+}
+
 __device__ __forceinline__ uint32_t div_clients(const EncodeArgs& a, uint32_t n) {
   if (a.div_l == 0) return n;  // nclients == 1
   const uint32_t t1 = __umulhi(n, a.div_m);
@@ -406,7 +417,7 @@ __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgc
 // the exclusive prefix (a root segment: body = stream bits before tile t).
 // pre1/pre2 (optional): this lane's status of tile t-1-lane, loaded earlier.
 __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int lane,
-                                        uint32_t* spin_err, bool& slow, bool have_pre = false,
+                                        bool& slow, bool have_pre = false,
                                         uint64_t pre1 = 0, uint64_t pre2 = 0) {
   Seg S = seg_identity();
   int64_t base = (int64_t)t - 1;
@@ -434,7 +445,7 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 24)) {  // safety net only: tickets guarantee progress
-        if (lane == 0) atomicOr(spin_err, 1u);
+        if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
         k = 0;
         w1 = kFlagPre;
         w2 = kFlagPre;
@@ -480,7 +491,7 @@ __device__ unsigned long long g_stamps[16];
 // tile).  Out of line: it keeps its registers off the common path.
 constexpr uint32_t kSegSlow = 0xFFFFFFFFu;  // lookback_deep's "a slow tile" result (has_nz)
 __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, int lane,
-                                          uint32_t* spin_err, uint64_t pre1, uint64_t pre2) {
+                                          uint64_t pre1, uint64_t pre2) {
   // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
   // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
   Seg S = seg_identity();  // fold of the newer windows already walked
@@ -503,7 +514,7 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 24)) {
-        if (lane == 0) atomicOr(spin_err, 1u);
+        if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
         Seg r = seg_identity();
         r.has_nz = 1;
         r.first = r.last = -1;
@@ -556,7 +567,7 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
     const uint32_t csum = (uint32_t)wave_sum_i((int32_t)contrib);
     if (__builtin_amdgcn_readlane(l1, 63) < 32u) {  // short newest body: exact scalar fold
       bool slow = false;
-      Seg r2 = lookback(status_c, t, lane, spin_err, slow);
+      Seg r2 = lookback(status_c, t, lane, slow);
       if (slow) r2.has_nz = kSegSlow;
       return r2;
     }
@@ -595,7 +606,7 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
 // newest tile's tail whenever that tile's body has >= 32 bits; otherwise the
 // scalar lookback() does the fold.  No prefix within 64 tiles: lookback_deep().
 __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t, int lane,
-                                            uint32_t* spin_err, bool& slow, uint64_t pre1,
+                                            bool& slow, uint64_t pre1,
                                             uint64_t pre2) {
   // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
   // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
@@ -614,7 +625,7 @@ __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t,
     const uint64_t val = __ballot(valid);
     if (pre == 0) {  // no prefix in the window: walk 64-tile windows
       FC_COUNT(10, 1);
-      Seg r = lookback_deep(status_c, t, lane, spin_err, pre1, pre2);
+      Seg r = lookback_deep(status_c, t, lane, pre1, pre2);
       if (r.has_nz == kSegSlow) {
         slow = true;
         r = seg_identity();
@@ -627,7 +638,7 @@ __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t,
     FC_COUNT(9, 1);
     __builtin_amdgcn_s_sleep(1);
     if (++spins > (1u << 24)) {
-      if (lane == 0) atomicOr(spin_err, 1u);
+      if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
       Seg r = seg_identity();
       r.has_nz = 1;
       r.first = r.last = -1;
@@ -682,7 +693,7 @@ __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t,
     return r;
   }
   FC_COUNT(11, 1);
-  return lookback(status_c, t, lane, spin_err, slow);  // short newest body: exact scalar fold
+  return lookback(status_c, t, lane, slow);  // short newest body: exact scalar fold
 }
 
 // Runtime-indexed read of a small register array without scratch (select chain).
@@ -1443,7 +1454,8 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         if (lane == 0) {
           st_agent(st + 1, kFlagSlow);
           st_agent(st, kFlagSlow);
-          if (atomicOr(&a.slow_flag[c], 1) == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = c;
+          const EncodeArgs& ka = enc_args_fresh();
+          if (atomicOr(&ka.slow_flag[c], 1) == 0) ka.slow_list[atomicAdd(ka.slow_count, 1u)] = c;
         }
         for (int i = lane; i < kWinWords; i += kEncThreads) win[i] = 0;
       } else {
@@ -1496,7 +1508,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         excl.has_nz = 1;
         excl.first = excl.last = -1;
       } else {
-        excl = lookback_vec(a.status + 2 * (int64_t)pc * a.T, pt, lane, a.spin_err, slow, pw1, pw2);
+        excl = lookback_vec(a.status + 2 * (int64_t)pc * a.T, pt, lane, slow, pw1, pw2);
         if (FC_ABL & 4096) {  // diagnostics: the look-back runs, its result is dropped
           asm volatile("" :: "s"((uint32_t)excl.body), "s"(excl.last), "s"(excl.tail));
           excl = seg_identity();
@@ -1508,7 +1520,10 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         if (lane == 0) {
           st_agent(st + 1, kFlagSlow);
           st_agent(st, kFlagSlow);
-          if (atomicOr(&a.slow_flag[pc], 1) == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = pc;
+          {
+            const EncodeArgs& ka = enc_args_fresh();
+            if (atomicOr(&ka.slow_flag[pc], 1) == 0) ka.slow_list[atomicAdd(ka.slow_count, 1u)] = pc;
+          }
         }
         for (int i = lane; i < kWinWords; i += kEncThreads) win[i] = 0;
       } else {
@@ -1536,7 +1551,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
           a.idx[ib + pt] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
           if (last_tile) {
             a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
-            a.total_bits[pc] = (int64_t)incl.body + trail_len;
+            enc_args_fresh().total_bits[pc] = (int64_t)incl.body + trail_len;
           }
           // leading pieces just before the body, trailing code after it
           emit64(win, tb, r0, kPre - bstart);
@@ -1550,7 +1565,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         const int64_t cap = cp.cap;
         uint32_t* out32 = cp.out;
         const uint64_t w0 = excl.body >> 5;
-        if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&a.overflow[pc], 1u);
+        if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&enc_args_fresh().overflow[pc], 1u);
         const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
         if (!(FC_ABL & 1024))
         for (uint32_t k = lane; k < nwords_owned; k += kEncThreads) {
@@ -1657,7 +1672,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
         st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
       }
       bool slow = false;
-      excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, a.spin_err, slow);
+      excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, slow);
     }
     const Seg incl = seg_combine(excl, agg);
     SlowEmit e;
