@@ -2188,83 +2188,176 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const float* dist_part, c
   }
 }
 
-// One-bit SGD (one_bit_sgd.py:56-81): pass 1 = masks + masked sums per client.
-__global__ __launch_bounds__(kThreads) void k_onebit_encode(const float* const* xs, int64_t P,
-                                                            float thr, uint32_t* masks, float* means,
-                                                            double* dist) {
-  __shared__ double r0[kThreads], r1[kThreads], r2[kThreads], r3[kThreads];
-  const int c = blockIdx.x;
-  const float* x = xs[c];
-  const int64_t nw = (P + 31) / 32;
-  uint32_t* m = masks + (int64_t)c * nw;
-  double sb = 0, sa = 0, nb = 0, na = 0;
-  for (int64_t w = threadIdx.x; w < nw; w += kThreads) {
-    uint32_t bits = 0;
-    for (int k = 0; k < 32; ++k) {
-      const int64_t i = w * 32 + k;
-      if (i >= P) break;
-      const float v = x[i] + 0.0f;
-      if (v < thr) {
-        sb += v;
-        nb += 1;
-      } else {
-        sa += v;
-        na += 1;
-        bits |= 1u << k;
-      }
-    }
-    m[w] = bits;
-  }
-  r0[threadIdx.x] = sb; r1[threadIdx.x] = sa; r2[threadIdx.x] = nb; r3[threadIdx.x] = na;
-  __syncthreads();
-  for (int o = kThreads / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      r0[threadIdx.x] += r0[threadIdx.x + o];
-      r1[threadIdx.x] += r1[threadIdx.x + o];
-      r2[threadIdx.x] += r2[threadIdx.x + o];
-      r3[threadIdx.x] += r3[threadIdx.x + o];
-    }
-    __syncthreads();
-  }
-  __shared__ float mb_s, ma_s;
-  if (threadIdx.x == 0) {
-    const float mb = (float)r0[0] / fmaxf((float)r2[0], 1.0f);
-    const float ma = (float)r1[0] / fmaxf((float)r3[0], 1.0f);
-    means[2 * c] = mb;
-    means[2 * c + 1] = ma;
-    mb_s = mb;
-    ma_s = ma;
-  }
-  __syncthreads();
-  double dd = 0;
-  for (int64_t i = threadIdx.x; i < P; i += kThreads) {
-    const float v = x[i] + 0.0f;
-    const float dec = (v < thr) ? mb_s : ma_s;
-    const float e = v - dec;
-    dd += (double)(e * e);
-  }
-  r0[threadIdx.x] = dd;
-  __syncthreads();
-  for (int o = kThreads / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) r0[threadIdx.x] += r0[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) dist[c] = r0[0];
+// One-bit SGD (one_bit_sgd.py:56-81).  One 256-thread workgroup per client;
+// each wave walks 2048-element tiles with fully coalesced 4-byte loads: lane l
+// reads element 64k + l of the tile (k = 0..31), so the ballot of (v >= thr) is
+// mask words 2k and 2k+1 directly (TF's mask_above_threshold, bit i of word w =
+// element 32w + i); lanes 2k / 2k+1 collect them by writelane and each tile
+// stores its 64 words in one coalesced store.  Pass 1 sums values above / all
+// (f32 per lane per tile, f64 beyond); the count above is the ballots'
+// popcount.  Pass 2 (after the means) re-reads the tensor for the distortion
+// sum of (v - decoded)^2, each term in float32 as TF computes it.  Reductions
+// are in a fixed order (deterministic).  Inputs pass through `+ 0.0f` so
+// denormals flush as on TF-CPU before the comparison.
+constexpr int kObThreads = 256;
+constexpr int kObWaves = kObThreads / 64;
+
+__device__ __forceinline__ double shfl_xor_f64(double v, int m) {
+  return __hiloint2double(__shfl_xor(__double2hiint(v), m), __shfl_xor(__double2loint(v), m));
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v += shfl_xor_f64(v, m);
+  return v;
 }
 
-__global__ void k_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t n,
-                                    int64_t P, float* out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P) return;
+__global__ __launch_bounds__(kObThreads) void k_onebit_encode(const float* const* xs, int64_t P,
+                                                              float thr, uint32_t* masks, float* means,
+                                                              double* dist) {
+  __shared__ double red[3][kObWaves];
+  __shared__ uint64_t redn[kObWaves];
+  __shared__ float mean_s[2];
+  const int c = blockIdx.x;
+  const float* __restrict__ x = xs[c];
   const int64_t nw = (P + 31) / 32;
-  float s = 0.0f;
-  for (int c = 0; c < n; ++c) {
-    const uint32_t bit = (masks[(int64_t)c * nw + (i >> 5)] >> (i & 31)) & 1u;
-    const float above = bit ? 1.0f : 0.0f;
-    const float dec = above * means[2 * c + 1] + (1.0f - above) * means[2 * c];
-    s = s + dec;
+  uint32_t* __restrict__ m = masks + (int64_t)c * nw;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t ntile = (P + 2047) / 2048;
+  double sa = 0.0, st = 0.0;
+  uint64_t na = 0;
+  // clients start at different tiles: rows share their alignment, and reading
+  // every client's same offset at once would load the same HBM channels
+  const int64_t t0 = ((int64_t)c * 977) % ntile;
+  for (int64_t tt = wv; tt < ntile; tt += kObWaves) {
+    const int64_t tile = tt + t0 < ntile ? tt + t0 : tt + t0 - ntile;
+    const int64_t base = tile * 2048;
+    const bool full = base + 2048 <= P;
+    const float* __restrict__ xt = x + base + lane;
+    float fa = 0.0f, ft = 0.0f;
+    uint32_t word = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // 8 loads in flight, then their 8 ballots
+      float raw[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        raw[j] = (full || base + 64 * k + lane < P) ? xt[64 * k] : 0.0f;
+      }
+      uint64_t bal[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        const bool in = full || base + 64 * k + lane < P;
+        const float v = raw[j] + 0.0f;
+        const bool ab = in && !(v < thr);
+        bal[j] = __ballot(ab);
+        na += (uint64_t)__popcll(bal[j]);
+        ft += v;
+        fa += ab ? v : 0.0f;
+      }
+      // mask words 16g .. 16g+15 into lanes 16g .. 16g+15.  The ballots' SGPRs were
+      // written by VALU compares: wait states before each v_writelane pair reads one
+      // (the compiler does not pad inline asm, and may place a compare right before)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2\n\tv_writelane_b32 %0, %3, %4"
+                     : "+v"(word)
+                     : "s"((uint32_t)bal[j]), "n"(2 * k), "s"((uint32_t)(bal[j] >> 32)), "n"(2 * k + 1));
+      }
+    }
+    if (tile * 64 + lane < nw) m[tile * 64 + lane] = word;
+    sa += (double)fa;
+    st += (double)ft;
   }
-  out[i] = s;
+  sa = wave_sum_f64(sa);
+  st = wave_sum_f64(st);
+  if (lane == 0) {
+    red[0][wv] = sa;
+    red[1][wv] = st;
+    redn[wv] = na;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a_ = 0.0, t_ = 0.0;
+    uint64_t n_ = 0;
+    for (int w = 0; w < kObWaves; ++w) {
+      a_ += red[0][w];
+      t_ += red[1][w];
+      n_ += redn[w];
+    }
+    const double b_ = t_ - a_;
+    const float mb = (float)b_ / fmaxf((float)(P - (int64_t)n_), 1.0f);
+    const float ma = (float)a_ / fmaxf((float)n_, 1.0f);
+    means[2 * c] = mb;
+    means[2 * c + 1] = ma;
+    mean_s[0] = mb;
+    mean_s[1] = ma;
+  }
+  __syncthreads();
+  const float mb = mean_s[0], ma = mean_s[1];
+  double dd = 0.0;
+  for (int64_t tt = wv; tt < ntile; tt += kObWaves) {
+    const int64_t tile = tt + t0 < ntile ? tt + t0 : tt + t0 - ntile;
+    const int64_t base = tile * 2048;
+    const bool full = base + 2048 <= P;
+    const float* __restrict__ xt = x + base + lane;
+    float fd = 0.0f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float raw[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        raw[j] = (full || base + 64 * k + lane < P) ? xt[64 * k] : 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        const float v = raw[j] + 0.0f;
+        const float e = v - ((v < thr) ? mb : ma);
+        // elements past P: v = 0 decodes to a mean, so the term is dropped
+        fd += (full || base + 64 * k + lane < P) ? e * e : 0.0f;
+      }
+    }
+    dd += (double)fd;
+  }
+  dd = wave_sum_f64(dd);
+  if (lane == 0) red[2][wv] = dd;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double d_ = 0.0;
+    for (int w = 0; w < kObWaves; ++w) d_ += red[2][w];
+    dist[c] = d_;
+  }
+}
+
+// Server sum (one_bit_sgd.py:87-112): one thread per mask word (32 elements);
+// clients in order, each decoded value exactly mask ? mean_above : mean_below
+// (TF's mask * ma + (1 - mask) * mb), summed in float32 as the reference's
+// accumulator.  The select is one bitop3 on the float bits.
+__global__ __launch_bounds__(256) void k_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t n,
+                                                           int64_t P, float* out) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nw = (P + 31) / 32;
+  if (w >= nw) return;
+  float s[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) s[k] = 0.0f;
+  for (int c = 0; c < n; ++c) {
+    const uint32_t bits = masks[(int64_t)c * nw + w];
+    const uint32_t mb = __float_as_uint(means[2 * c]), ma = __float_as_uint(means[2 * c + 1]);
+    const uint32_t dx = ma ^ mb;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const uint32_t sel = (uint32_t)(((int32_t)(bits << (31 - k))) >> 31);  // all ones if bit k
+      s[k] = s[k] + __uint_as_float(mb ^ (dx & sel));
+    }
+  }
+  const int64_t e0 = w * 32;
+#pragma unroll
+  for (int k = 0; k < 32; ++k)
+    if (e0 + k < P) out[e0 + k] = s[k];
 }
 
 
@@ -2933,7 +3026,7 @@ int fc_onebit_encode(const float* const* xs, int32_t nclients, int64_t P, float 
                      float* means, double* dist, void* stream) {
   if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
   if (!xs || !masks || !means || !dist) return fail(-1, "null pointer");
-  hipLaunchKernelGGL(k_onebit_encode, dim3(nclients), dim3(kThreads), 0, (hipStream_t)stream, xs, P, threshold,
+  hipLaunchKernelGGL(k_onebit_encode, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, threshold,
                      masks, means, dist);
   return check_launch("k_onebit_encode");
 }
@@ -2942,7 +3035,8 @@ int fc_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t ncli
                          void* stream) {
   if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
   if (!masks || !means || !out) return fail(-1, "null pointer");
-  hipLaunchKernelGGL(k_onebit_decode_sum, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  const int64_t nw = (P + 31) / 32;
+  hipLaunchKernelGGL(k_onebit_decode_sum, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      masks, means, nclients, P, out);
   return check_launch("k_onebit_decode_sum");
 }
