@@ -2211,9 +2211,13 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
-__global__ __launch_bounds__(kObThreads) void k_onebit_encode(const float* const* xs, int64_t P,
-                                                              float thr, uint32_t* masks, float* means,
-                                                              double* dist) {
+// KIND 0: one-bit SGD (threshold thr, class means).  KIND 1: DRIVE
+// (drive.py:58-76: mask = !(x < 0), scale from sum |x| and sum x^2, means
+// -scale / +scale); the same two passes, only the sums and the means differ.
+template <int KIND>
+__global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* xs, int64_t P, float thr,
+                                                            int min_distortion, uint32_t* masks,
+                                                            float* means, double* dist) {
   __shared__ double red[3][kObWaves];
   __shared__ uint64_t redn[kObWaves];
   __shared__ float mean_s[2];
@@ -2252,8 +2256,13 @@ __global__ __launch_bounds__(kObThreads) void k_onebit_encode(const float* const
         const bool ab = in && !(v < thr);
         bal[j] = __ballot(ab);
         na += (uint64_t)__popcll(bal[j]);
-        ft += v;
-        fa += ab ? v : 0.0f;
+        if (KIND == 0) {  // sum above threshold, sum of all
+          ft += v;
+          fa += ab ? v : 0.0f;
+        } else {  // sum |x|, sum x^2
+          fa += fabsf(v);
+          ft += v * v;
+        }
       }
       // mask words 16g .. 16g+15 into lanes 16g .. 16g+15.  The ballots' SGPRs were
       // written by VALU compares: wait states before each v_writelane pair reads one
@@ -2286,9 +2295,23 @@ __global__ __launch_bounds__(kObThreads) void k_onebit_encode(const float* const
       t_ += red[1][w];
       n_ += redn[w];
     }
-    const double b_ = t_ - a_;
-    const float mb = (float)b_ / fmaxf((float)(P - (int64_t)n_), 1.0f);
-    const float ma = (float)a_ / fmaxf((float)n_, 1.0f);
+    float mb, ma;
+    if (KIND == 0) {
+      mb = (float)(t_ - a_) / fmaxf((float)(P - (int64_t)n_), 1.0f);
+      ma = (float)a_ / fmaxf((float)n_, 1.0f);
+    } else {
+      const float norm1 = (float)a_;
+      float scale;
+      if (min_distortion) {
+        scale = norm1 / (float)P;  // drive.py:61-62
+      } else {
+        const float norm2 = (float)sqrt(t_);
+        const float n2sq = norm2 * norm2;
+        scale = norm1 == 0.0f ? 0.0f : n2sq / norm1;  // drive.py:63-65 (divide_no_nan)
+      }
+      mb = -scale;
+      ma = scale;
+    }
     means[2 * c] = mb;
     means[2 * c + 1] = ma;
     mean_s[0] = mb;
@@ -2512,77 +2535,6 @@ __global__ __launch_bounds__(256) void k_vote_finalize(VoteArgs a) {
     a.bits[ck] = (int64_t)total;
     a.dist[ck] = rdist[0];
   }
-}
-
-
-// ---------------------------------------------------------------------------
-// DRIVE (comparison_methods/drive.py:58-76): per client the sign mask (bit set
-// = non-negative), scale = ||x||_2^2 / ||x||_1 (unbiased, divide_no_nan) or
-// ||x||_1 / P (min_distortion) in float32 from float64 sums, and the
-// distortion sum (x - (+-scale))^2.  The server sum reuses k_onebit_decode_sum
-// with (below, above) = (-scale, +scale).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void k_drive_encode(const float* const* xs, int64_t P, int min_distortion,
-                                                           uint32_t* masks, float* means, double* dist) {
-  __shared__ double r0[kThreads], r1[kThreads];
-  __shared__ float scale_s;
-  const int c = blockIdx.x;
-  const float* x = xs[c];
-  const int64_t nw = (P + 31) / 32;
-  uint32_t* m = masks + (int64_t)c * nw;
-  double sa = 0, sq = 0;
-  for (int64_t w = threadIdx.x; w < nw; w += kThreads) {
-    uint32_t bits = 0;
-    for (int k = 0; k < 32; ++k) {
-      const int64_t i = w * 32 + k;
-      if (i >= P) break;
-      const float v = x[i] + 0.0f;  // DAZ
-      sa += fabs((double)v);
-      sq += (double)v * (double)v;
-      if (!(v < 0.0f)) bits |= 1u << k;  // mask_negatives = x < 0 (drive.py:59)
-    }
-    m[w] = bits;
-  }
-  r0[threadIdx.x] = sa;
-  r1[threadIdx.x] = sq;
-  __syncthreads();
-  for (int o = kThreads / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      r0[threadIdx.x] += r0[threadIdx.x + o];
-      r1[threadIdx.x] += r1[threadIdx.x + o];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const float norm1 = (float)r0[0];
-    float scale;
-    if (min_distortion) {
-      scale = norm1 / (float)P;                       // drive.py:61-62
-    } else {
-      const float norm2 = (float)sqrt(r1[0]);
-      const float n2sq = norm2 * norm2;
-      scale = norm1 == 0.0f ? 0.0f : n2sq / norm1;     // drive.py:63-65 (divide_no_nan)
-    }
-    means[2 * c] = -scale;
-    means[2 * c + 1] = scale;
-    scale_s = scale;
-  }
-  __syncthreads();
-  const float sc = scale_s;
-  double dd = 0;
-  for (int64_t i = threadIdx.x; i < P; i += kThreads) {
-    const float v = x[i] + 0.0f;
-    const float dec = (v < 0.0f) ? -sc : sc;
-    const float e = v - dec;
-    dd += (double)(e * e);
-  }
-  r0[threadIdx.x] = dd;
-  __syncthreads();
-  for (int o = kThreads / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) r0[threadIdx.x] += r0[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) dist[c] = r0[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -2958,9 +2910,9 @@ int fc_drive_encode(const float* const* xs, int32_t nclients, int64_t P, int min
                     float* means, double* dist, void* stream) {
   if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
   if (!xs || !masks || !means || !dist) return fail(-1, "null pointer");
-  hipLaunchKernelGGL(k_drive_encode, dim3(nclients), dim3(kThreads), 0, (hipStream_t)stream, xs, P,
+  hipLaunchKernelGGL(k_mask_encode<1>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, 0.0f,
                      min_distortion, masks, means, dist);
-  return check_launch("k_drive_encode");
+  return check_launch("k_mask_encode<1>");
 }
 
 int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, int64_t seed0, int64_t seed1,
@@ -3026,9 +2978,9 @@ int fc_onebit_encode(const float* const* xs, int32_t nclients, int64_t P, float 
                      float* means, double* dist, void* stream) {
   if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
   if (!xs || !masks || !means || !dist) return fail(-1, "null pointer");
-  hipLaunchKernelGGL(k_onebit_encode, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, threshold,
-                     masks, means, dist);
-  return check_launch("k_onebit_encode");
+  hipLaunchKernelGGL(k_mask_encode<0>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, threshold,
+                     0, masks, means, dist);
+  return check_launch("k_mask_encode<0>");
 }
 
 int fc_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t nclients, int64_t P, float* out,

@@ -1,4 +1,4 @@
-"""Diagnostic: time the one-bit SGD codec (fc_onebit_encode + fc_onebit_decode_sum) on C x P."""
+"""Diagnostic: time the one-bit SGD codec (fc_onebit_encode + fc_onebit_decode_sum) and DRIVE encode on C x P."""
 import os
 import sys
 import time
@@ -25,5 +25,8 @@ for it in range(3):
   out = codec.onebit_decode_sum(masks, means, C, P)
   torch.cuda.synchronize()
   t2 = time.perf_counter()
-  print("onebit C=%d P=%d: encode %.2f ms (%.0f GB/s fp32 read), decode-sum %.2f ms" % (
-      C, P, (t1 - t0) * 1e3, C * P * 4 / (t1 - t0) / 1e9, (t2 - t1) * 1e3))
+  codec.drive_encode(rows)
+  torch.cuda.synchronize()
+  t3 = time.perf_counter()
+  print("onebit C=%d P=%d: encode %.2f ms (%.0f GB/s fp32 read), decode-sum %.2f ms, DRIVE encode %.2f ms" % (
+      C, P, (t1 - t0) * 1e3, C * P * 4 / (t1 - t0) / 1e9, (t2 - t1) * 1e3, (t3 - t2) * 1e3))
