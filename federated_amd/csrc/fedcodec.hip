@@ -2129,35 +2129,69 @@ __global__ void k_noise_sum(const int64_t* __restrict__ seeds, int32_t n, int64_
 }
 
 // Per-client norm: one workgroup per client, float64 accumulation, fixed order.
-__global__ __launch_bounds__(kThreads) void k_client_norms(const float* const* xs, int64_t P,
-                                                           int kind, float* norms) {
-  __shared__ double red[kThreads];
+__device__ __forceinline__ double shfl_xor_f64(double v, int m) {
+  return __hiloint2double(__shfl_xor(__double2hiint(v), m), __shfl_xor(__double2loint(v), m));
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v += shfl_xor_f64(v, m);
+  return v;
+}
+
+// Per-client normaliser / norm: one 1024-thread workgroup per client (enough
+// waves per CU even for a few hundred clients); each wave reads 2048-element
+// tiles with coalesced 4-byte loads, 8 in flight.  Max is exact in float32;
+// sums go through float32 per-lane tile partials (32 elements) into float64,
+// reduced in a fixed order.  Inputs pass through `+ 0.0f` (DAZ as TF-CPU).
+constexpr int kNormThreads = 1024;
+__global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* const* xs, int64_t P,
+                                                               int kind, float* norms) {
+  __shared__ double red[kNormThreads / 64];
   const int c = blockIdx.x;
-  const float* x = xs[c];
+  const float* __restrict__ x = xs[c];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool is_max = kind == FC_NORM_MAX_MAGNITUDE || kind == FC_NORM_LINF;
+  const bool is_abs = kind == FC_NORM_MEAN_MAGNITUDE;
+  const int64_t ntile = (P + 2047) / 2048;
   double acc = 0.0;
-  for (int64_t i = threadIdx.x; i < P; i += kThreads) {
-    const float v = x[i] + 0.0f;  // DAZ
-    const double a = fabs((double)v);
-    if (kind == FC_NORM_MAX_MAGNITUDE || kind == FC_NORM_LINF) acc = a > acc ? a : acc;
-    else if (kind == FC_NORM_MEAN_MAGNITUDE) acc += a;
-    else acc += a * a;
-  }
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int o = kThreads / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      const double b = red[threadIdx.x + o];
-      red[threadIdx.x] = (kind == FC_NORM_MAX_MAGNITUDE || kind == FC_NORM_LINF) ? fmax(red[threadIdx.x], b)
-                                                                               : red[threadIdx.x] + b;
+  float mx = 0.0f;
+  for (int64_t tile = wv; tile < ntile; tile += kNormThreads / 64) {
+    const int64_t base = tile * 2048;
+    const bool full = base + 2048 <= P;
+    const float* __restrict__ xt = x + base + lane;
+    float part = 0.0f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float raw[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        raw[j] = (full || base + 64 * k + lane < P) ? xt[64 * k] : 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = fabsf(raw[j] + 0.0f);
+        mx = fmaxf(mx, a);
+        part += is_abs ? a : a * a;
+      }
     }
-    __syncthreads();
+    acc += (double)part;
   }
+  double r = is_max ? (double)mx : acc;
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) {
+    const double o = shfl_xor_f64(r, m);
+    r = is_max ? fmax(r, o) : r + o;
+  }
+  if (lane == 0) red[wv] = r;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    double r = red[0];
-    if (kind == FC_NORM_MEAN_MAGNITUDE) r = r / (double)P;
-    if (kind == FC_NORM_DIMENSIONLESS) r = sqrt(r / (double)P);
-    if (kind == FC_NORM_L2) r = sqrt(r);
-    norms[c] = (float)r;
+    double t = red[0];
+    for (int w = 1; w < kNormThreads / 64; ++w) t = is_max ? fmax(t, red[w]) : t + red[w];
+    if (kind == FC_NORM_MEAN_MAGNITUDE) t = t / (double)P;
+    if (kind == FC_NORM_DIMENSIONLESS) t = sqrt(t / (double)P);
+    if (kind == FC_NORM_L2) t = sqrt(t);
+    norms[c] = (float)t;
   }
 }
 
@@ -2202,14 +2236,6 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const float* dist_part, c
 constexpr int kObThreads = 256;
 constexpr int kObWaves = kObThreads / 64;
 
-__device__ __forceinline__ double shfl_xor_f64(double v, int m) {
-  return __hiloint2double(__shfl_xor(__double2hiint(v), m), __shfl_xor(__double2loint(v), m));
-}
-__device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) v += shfl_xor_f64(v, m);
-  return v;
-}
 
 // KIND 0: one-bit SGD (threshold thr, class means).  KIND 1: DRIVE
 // (drive.py:58-76: mask = !(x < 0), scale from sum |x| and sum x^2, means
@@ -2962,7 +2988,8 @@ int fc_client_norms(const float* const* xs, int32_t nclients, int64_t P, int kin
   if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
   if (kind < 1 || kind > 5) return fail(-1, "bad norm kind");
   if (!xs || !norms) return fail(-1, "null pointer");
-  hipLaunchKernelGGL(k_client_norms, dim3(nclients), dim3(kThreads), 0, (hipStream_t)stream, xs, P, kind, norms);
+  hipLaunchKernelGGL(k_client_norms, dim3(nclients), dim3(kNormThreads), 0, (hipStream_t)stream, xs, P, kind,
+                     norms);
   return check_launch("k_client_norms");
 }
 

@@ -1,0 +1,44 @@
+"""Diagnostic: time the auxiliary kernels of the §8 rows at bench-like sizes.
+
+client norms (QSGD / wrappers), dithered noise sum, step-size vote lengths,
+Hadamard rotation.  Prints ms and the fp32-read rate of each.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from federated_amd import _lib, codec  # noqa: E402
+
+dev = torch.device("cuda:0")
+
+
+def timed(name, fn, nbytes, reps=3):
+  fn()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(reps):
+    fn()
+  torch.cuda.synchronize()
+  dt = (time.perf_counter() - t0) / reps
+  print("%-34s %9.2f ms  %7.0f GB/s" % (name, dt * 1e3, nbytes / dt / 1e9), flush=True)
+
+
+P = 25_000_000
+C = int(os.environ.get("C", 256))
+g = torch.Generator(device=dev)
+rows = []
+for c in range(C):
+  g.manual_seed(11 + c)
+  rows.append(torch.randn(P, generator=g, device=dev))
+seeds = torch.tensor([[c, c + 1] for c in range(C)], dtype=torch.int64, device=dev)
+timed("client_norms L2 (C x 25M)", lambda: codec.client_norms(rows, _lib.NORM_L2), C * P * 4)
+timed("noise_sum dithered (C x 25M)", lambda: codec.noise_sum(seeds, P, dev), P * 4)
+timed("vote_lengths K=4 (64 x 25M)",
+      lambda: codec.vote_lengths(rows[:64], np.array([0.25, 0.5, 1.0, 2.0], np.float32), seeds[:64],
+                                 _lib.STOCHASTIC), 64 * P * 4, reps=1)
+H = [torch.randn(1 << 24, generator=g, device=dev) for _ in range(64)]
+timed("hadamard 64 x 2^24 (fwd)", lambda: codec.hadamard_(H, (1, 2)), 64 * (1 << 24) * 4 * 2)
