@@ -2109,20 +2109,37 @@ __global__ void k_dequantize(const int32_t* __restrict__ s, int64_t P, float ste
   out[i] = f * step;
 }
 
-__global__ void k_noise_sum(const int64_t* __restrict__ seeds, int32_t n, int64_t P,
-                            float* __restrict__ out) {
+// noise_sum[i] = sum over clients, in client order, of TF's dither noise
+// u01 - 0.5 for element i.  Each workgroup scrambles a chunk of 256 clients'
+// seeds into Philox keys once (LDS); every thread then draws one Philox group
+// (4 elements) per client with the key uniform across the wave (round keys on
+// the scalar unit, as in the encoder).
+__global__ __launch_bounds__(256) void k_noise_sum(const int64_t* __restrict__ seeds, int32_t n, int64_t P,
+                                                   float* __restrict__ out) {
+  __shared__ Key4 keys[256];
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t e0 = g * 4;
-  if (e0 >= P) return;
   float s[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int c = 0; c < n; ++c) {
-    const Key4 key = tf_seed_scramble(seeds[2 * c], seeds[2 * c + 1]);
-    const uint4 rb = philox_group(key, (uint32_t)g);
-    s[0] = s[0] + (u01(rb.x) - 0.5f);
-    s[1] = s[1] + (u01(rb.y) - 0.5f);
-    s[2] = s[2] + (u01(rb.z) - 0.5f);
-    s[3] = s[3] + (u01(rb.w) - 0.5f);
+  for (int c0 = 0; c0 < n; c0 += 256) {
+    __syncthreads();
+    if (c0 + (int)threadIdx.x < n)
+      keys[threadIdx.x] = tf_seed_scramble(seeds[2 * (c0 + threadIdx.x)], seeds[2 * (c0 + threadIdx.x) + 1]);
+    __syncthreads();
+    const int cn = min(256, n - c0);
+    for (int j = 0; j < cn; ++j) {
+      Key4 key = keys[j];
+      key.k0 = __builtin_amdgcn_readfirstlane(key.k0);
+      key.k1 = __builtin_amdgcn_readfirstlane(key.k1);
+      key.c2 = __builtin_amdgcn_readfirstlane(key.c2);
+      key.c3 = __builtin_amdgcn_readfirstlane(key.c3);
+      const uint4 rb = philox_group_u(key, (uint32_t)g);
+      s[0] = s[0] + (u01(rb.x) - 0.5f);
+      s[1] = s[1] + (u01(rb.y) - 0.5f);
+      s[2] = s[2] + (u01(rb.z) - 0.5f);
+      s[3] = s[3] + (u01(rb.w) - 0.5f);
+    }
   }
+  if (e0 >= P) return;
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     if (e0 + k < P) out[e0 + k] = s[k];
