@@ -2596,43 +2596,73 @@ __device__ __forceinline__ float rademacher(const Key4& key, int64_t i) {
   return (w >> 31) ? -1.0f : 1.0f;
 }
 
+__device__ __forceinline__ float sign_of(uint32_t w) { return (w >> 31) ? -1.0f : 1.0f; }
+
 __global__ __launch_bounds__(256) void k_fwht_pass(float* const* rows, int64_t n, int L0, int k, int sign_in,
                                                    int sign_out, float scale, int64_t seed0, int64_t seed1) {
-  __shared__ float buf[4096];
-  const int64_t G = (int64_t)1 << k;               // rows of a group
-  const int64_t gsize = G * (L0 == 0 ? 1 : (4096 >> k));
-  const int64_t C = gsize >> k;                    // consecutive columns per group
-  const int64_t S = (int64_t)1 << L0;              // row stride
-  const int64_t per_row = n / gsize;               // groups per client row
-  const int64_t c = blockIdx.x / per_row;
-  const int64_t g = blockIdx.x - c * per_row;
-  const int64_t nblk = S / C;                      // column blocks below the levels
-  const int64_t hi = g / nblk, cb = g - hi * nblk;
-  const int64_t base = hi * (S << k) + cb * C;
+  __shared__ __attribute__((aligned(16))) float buf[4096];
+  // every size is a power of two: index arithmetic by shifts and masks
+  const int lg = L0 == 0 ? k : 12;                 // log2 group size
+  const int lC = lg - k;                           // log2 consecutive columns per group
+  const int64_t gsize = (int64_t)1 << lg;
+  const int64_t C = (int64_t)1 << lC;
+  const int lrow = 63 - __clzll((unsigned long long)(n >> lg));  // log2 groups per client row
+  const int64_t c = (int64_t)blockIdx.x >> lrow;
+  const int64_t g = (int64_t)blockIdx.x & (((int64_t)1 << lrow) - 1);
+  const int lnblk = L0 - lC;                       // log2 column blocks below the levels (pass > 0)
+  const int64_t hi = L0 == 0 ? g : g >> lnblk, cb = L0 == 0 ? 0 : g & (((int64_t)1 << lnblk) - 1);
+  const int64_t base = L0 == 0 ? g << lg : (hi << (L0 + k)) + (cb << lC);
   float* x = rows[c];
   const Key4 key = tf_seed_scramble(seed0, seed1);
-  for (int64_t t = threadIdx.x; t < gsize; t += 256) {
-    const int64_t e = base + (t / C) * S + (t % C);
-    float v = x[e];
-    if (sign_in) v *= rademacher(key, e);
-    buf[t] = v;
+  // element of group index t: row t >> lC at stride 2^L0, column t & (C - 1)
+  if (gsize >= 1024) {  // 4 consecutive elements per thread (C >= 4): float4 and one Philox group
+    for (int64_t t = 4 * threadIdx.x; t < gsize; t += 1024) {
+      const int64_t e = base + ((t >> lC) << L0) + (t & (C - 1));
+      float4 v = *(const float4*)(x + e);
+      if (sign_in) {
+        const uint4 r = philox_group(key, (uint32_t)(e >> 2));
+        v.x *= sign_of(r.x); v.y *= sign_of(r.y); v.z *= sign_of(r.z); v.w *= sign_of(r.w);
+      }
+      *(float4*)(buf + t) = v;
+    }
+  } else {
+    for (int64_t t = threadIdx.x; t < gsize; t += 256) {
+      const int64_t e = base + ((t >> lC) << L0) + (t & (C - 1));
+      float v = x[e];
+      if (sign_in) v *= rademacher(key, e);
+      buf[t] = v;
+    }
   }
   __syncthreads();
   for (int j = 0; j < k; ++j) {
-    const int64_t h = C << j;  // partner distance in buf
-    for (int64_t b = threadIdx.x; b < gsize / 2; b += 256) {
-      const int64_t lo = (b / h) * 2 * h + (b % h);
+    const int lh = lC + j;  // partner distance 2^lh in buf
+    const int64_t h = (int64_t)1 << lh;
+    for (int64_t b2 = threadIdx.x; b2 < gsize / 2; b2 += 256) {
+      const int64_t lo = ((b2 >> lh) << (lh + 1)) + (b2 & (h - 1));
       const float u = buf[lo], w = buf[lo + h];
       buf[lo] = u + w;
       buf[lo + h] = u - w;
     }
     __syncthreads();
   }
-  for (int64_t t = threadIdx.x; t < gsize; t += 256) {
-    const int64_t e = base + (t / C) * S + (t % C);
-    float v = buf[t] * scale;
-    if (sign_out) v *= rademacher(key, e);
-    x[e] = v;
+  if (gsize >= 1024) {
+    for (int64_t t = 4 * threadIdx.x; t < gsize; t += 1024) {
+      const int64_t e = base + ((t >> lC) << L0) + (t & (C - 1));
+      float4 v = *(const float4*)(buf + t);
+      v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+      if (sign_out) {
+        const uint4 r = philox_group(key, (uint32_t)(e >> 2));
+        v.x *= sign_of(r.x); v.y *= sign_of(r.y); v.z *= sign_of(r.z); v.w *= sign_of(r.w);
+      }
+      *(float4*)(x + e) = v;
+    }
+  } else {
+    for (int64_t t = threadIdx.x; t < gsize; t += 256) {
+      const int64_t e = base + ((t >> lC) << L0) + (t & (C - 1));
+      float v = buf[t] * scale;
+      if (sign_out) v *= rademacher(key, e);
+      x[e] = v;
+    }
   }
 }
 
