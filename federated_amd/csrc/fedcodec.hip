@@ -2469,17 +2469,31 @@ __global__ __launch_bounds__(64) void k_vote_tiles(VoteArgs a) {
     const float* x = a.xs[c];
     float xv[16];
     uint32_t rb[16];
+    if (tile_base + kTE <= a.P && ((uintptr_t)x & 15u) == 0) {  // full, aligned tile: 4 x 16 B per lane
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int64_t e = tile_base + 16 * lane + i;
-      xv[i] = e < a.P ? x[e] : 0.0f;
+      for (int g = 0; g < 4; ++g) {
+        const float4 v = *(const float4*)(x + tile_base + 16 * lane + 4 * g);
+        xv[4 * g] = v.x; xv[4 * g + 1] = v.y; xv[4 * g + 2] = v.z; xv[4 * g + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t e = tile_base + 16 * lane + i;
+        xv[i] = e < a.P ? x[e] : 0.0f;
+      }
     }
     Key4 key{0, 0, 0, 0};
-    if (MODE != FC_UNIFORM) key = tf_seed_scramble(a.seeds[2 * c], a.seeds[2 * c + 1]);
+    if (MODE != FC_UNIFORM) {
+      key = tf_seed_scramble(a.seeds[2 * c], a.seeds[2 * c + 1]);
+      key.k0 = __builtin_amdgcn_readfirstlane(key.k0);  // wave-uniform: scalar-unit round keys
+      key.k1 = __builtin_amdgcn_readfirstlane(key.k1);
+      key.c2 = __builtin_amdgcn_readfirstlane(key.c2);
+      key.c3 = __builtin_amdgcn_readfirstlane(key.c3);
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       uint4 r = make_uint4(0, 0, 0, 0);
-      if (MODE != FC_UNIFORM) r = philox_group(key, (uint32_t)((tile_base + 16 * lane + 4 * g) >> 2));
+      if (MODE != FC_UNIFORM) r = philox_group_u(key, (uint32_t)((tile_base + 16 * lane + 4 * g) >> 2));
       rb[4 * g] = r.x; rb[4 * g + 1] = r.y; rb[4 * g + 2] = r.z; rb[4 * g + 3] = r.w;
     }
     for (int k = 0; k < a.K; ++k) {
@@ -2504,14 +2518,14 @@ __global__ __launch_bounds__(64) void k_vote_tiles(VoteArgs a) {
           prev = rel;
         }
       }
-      const int32_t im = wave_incl_max(prev, lane);
-      const int32_t lprev = __shfl_up(im, 1, 64);
+      const int32_t im = dpp_incl_max(prev);
+      const int32_t lprev = dpp_shr1(im, -1);
       const uint32_t R = (lfirst >= 0 && lane > 0 && lprev >= 0) ? glen((uint32_t)(lfirst - lprev)) : 0u;
       const uint32_t body = (uint32_t)wave_sum_i((int32_t)(len + R));
       const float d = wave_sum_f(dist);
       const uint64_t fm = __ballot(lfirst >= 0);
-      const int32_t tfirst = __shfl(lfirst, fm ? (int)__builtin_ctzll(fm) : 0, 64);
-      const int32_t tlast = __shfl(im, 63, 64);
+      const int32_t tfirst = __builtin_amdgcn_readlane(lfirst, fm ? (int)__builtin_ctzll(fm) : 0);
+      const int32_t tlast = lane63(im);
       if (lane == 0) {
         VoteRec r;
         r.body = body;
