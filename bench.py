@@ -17,7 +17,13 @@ on device, and resident in HBM before the timed region starts; the delta pool
 beyond the 256 MiB Infinity Cache, so every client streams from HBM.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--clients C]
-       [--mode stochastic|uniform|dithered] [--no-cpu-baseline]
+       [--mode stochastic|uniform|dithered] [--no-cpu-baseline] [--slabs S]
+       [--dump-result PATH]
+
+N > 1: each rank decodes its clients in S tile ranges and all-reduces each range
+while the next decodes.  Rehearsal on a 1-GPU box (never used by the driver):
+FEDCODEC_BENCH_BACKEND=gloo FEDCODEC_BENCH_ONE_DEVICE=1 with --dump-result, see
+tools/rehearse_multigpu.sh.
 """
 import argparse
 import json
