@@ -240,31 +240,6 @@ __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
 // ---------------------------------------------------------------------------
-// Wave-level scans (64 lanes).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int32_t wave_incl_max(int32_t v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v = max(v, t);
-  }
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
-  return v;
-}
-__device__ __forceinline__ int32_t wave_min(int32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-// ---------------------------------------------------------------------------
 // Encoder.
 // ---------------------------------------------------------------------------
 struct EncodeArgs {
@@ -338,13 +313,6 @@ __device__ __forceinline__ void win_emit(uint32_t* win, uint64_t v, uint32_t L, 
   }
 }
 
-// Bits of stream word k covered by a piece (v, L) starting at bit p (MSB-first).
-__device__ __forceinline__ uint32_t piece_word(uint64_t v, uint32_t L, uint32_t p, uint32_t k) {
-  const int32_t lo = 32 * (int32_t)k, end = (int32_t)(p + L);
-  if (L == 0 || end <= lo || (int32_t)p >= lo + 32) return 0;
-  const int32_t sh = lo + 32 - end;
-  return sh >= 0 ? (uint32_t)(sh >= 64 ? 0 : v << sh) : (uint32_t)(-sh >= 64 ? 0 : v >> -sh);
-}
 
 // OR the part of a piece (ending at body position `end`) that falls in the last
 // 32 body bits into the tail word.
@@ -1037,32 +1005,6 @@ __device__ __forceinline__ uint32_t win_bits32(const uint32_t* win, uint32_t s) 
   return (uint32_t)(pair >> (32u - o));
 }
 
-// Four interleaved inclusive DPP scans (independent chains hide the DPP hazard).
-__device__ __forceinline__ void dpp_incl_max4(int32_t (&x)[4]) {
-  const int32_t id = (int32_t)0x80000000;
-#define FC_MAXSTEP(ctl, rm)                                                                  \
-  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                             \
-      x[j] = max(x[j], __builtin_amdgcn_update_dpp(id, x[j], ctl, rm, 0xf, false));
-  FC_MAXSTEP(0x111, 0xf)
-  FC_MAXSTEP(0x112, 0xf)
-  FC_MAXSTEP(0x114, 0xf)
-  FC_MAXSTEP(0x118, 0xf)
-  FC_MAXSTEP(0x142, 0xa)
-  FC_MAXSTEP(0x143, 0xc)
-#undef FC_MAXSTEP
-}
-__device__ __forceinline__ void dpp_incl_sum2(uint32_t (&x)[2]) {
-#define FC_SUMSTEP(ctl, rm)                                                                  \
-  _Pragma("unroll") for (int j = 0; j < 2; ++j)                                             \
-      x[j] += __builtin_amdgcn_update_dpp(0u, x[j], ctl, rm, 0xf, false);
-  FC_SUMSTEP(0x111, 0xf)
-  FC_SUMSTEP(0x112, 0xf)
-  FC_SUMSTEP(0x114, 0xf)
-  FC_SUMSTEP(0x118, 0xf)
-  FC_SUMSTEP(0x142, 0xa)
-  FC_SUMSTEP(0x143, 0xc)
-#undef FC_SUMSTEP
-}
 
 // Exact path (clients with a rare tile: a code past the fast path's limits or
 // a body larger than the LDS window), run by k_encode_exact after k_encode so
@@ -1207,7 +1149,6 @@ __device__ __forceinline__ void slow_emit(const EncodeArgs& a, const ClientQ& cq
 
 // s_waitcnt immediates (gfx9 encoding): vmcnt(0) alone / lgkmcnt(0) alone.
 constexpr int kWaitVm0 = 0x0F70;
-constexpr int kWaitLgkm0 = 0xC07F;
 
 // Tile staging through LDS-DMA (global_load_lds_dwordx4).  DMA instruction b
 // (b = 0..3) fetches the tile's 1-KiB global block b -- coalesced -- into staging
