@@ -340,3 +340,46 @@ def test_drive_with_hadamard_rotation_end_to_end(gpu):
   # unweighted mean of the clients, approximated by 1-bit DRIVE in the rotated basis
   mean = np.mean(np.stack(xs), axis=0)
   assert np.linalg.norm(res - mean) < np.linalg.norm(mean) * 1.5
+
+
+@pytest.mark.parametrize("P", [1, 31, 2047, 2049, 70_001])
+def test_mask_encoders_many_tiles(gpu, P):
+  """k_mask_encode (one-bit SGD, DRIVE) over full and partial 2048-element tiles:
+  masks bit-exact (bit i of word w = element 32w + i), means and distortion
+  against float64 numpy within float32 tolerance; client_norms likewise."""
+  rng = np.random.default_rng(P)
+  xs = [(rng.standard_normal(P) * (1 + c)).astype(np.float32) for c in range(3)]
+  xs[1][: P // 2] = 0.0
+  dev = [torch.from_numpy(x).to(gpu) for x in xs]
+  nw = (P + 31) // 32
+
+  def want_masks(ab):
+    bits = np.zeros(nw * 32, bool)
+    bits[:P] = ab
+    return np.packbits(bits.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").ravel().astype(np.uint32)
+
+  masks, means, dist = codec.onebit_encode(dev, 0.1)
+  masks = masks.cpu().numpy().view(np.uint32).reshape(3, nw)
+  means = means.cpu().numpy().reshape(3, 2)
+  for c, x in enumerate(xs):
+    ab = ~(x < np.float32(0.1))
+    np.testing.assert_array_equal(masks[c], want_masks(ab))
+    mb = x[~ab].astype(np.float64).sum() / max((~ab).sum(), 1)
+    ma = x[ab].astype(np.float64).sum() / max(ab.sum(), 1)
+    np.testing.assert_allclose(means[c], [mb, ma], rtol=1e-5, atol=1e-7)
+    dec = np.where(ab, means[c, 1], means[c, 0]).astype(np.float32)
+    np.testing.assert_allclose(float(dist[c]), float(((x - dec).astype(np.float64) ** 2).sum()), rtol=1e-5)
+
+  masks, means, dist = codec.drive_encode(dev)
+  masks = masks.cpu().numpy().view(np.uint32).reshape(3, nw)
+  means = means.cpu().numpy().reshape(3, 2)
+  for c, x in enumerate(xs):
+    np.testing.assert_array_equal(masks[c], want_masks(~(x < 0)))
+    n1 = np.abs(x.astype(np.float64)).sum()
+    scale = (np.sqrt((x.astype(np.float64) ** 2).sum()) ** 2 / n1) if n1 else 0.0
+    np.testing.assert_allclose(means[c], [-scale, scale], rtol=1e-5)
+
+  for kind, fn in ((_lib.NORM_L2, lambda x: np.sqrt((x.astype(np.float64) ** 2).sum())),
+                   (_lib.NORM_MAX_MAGNITUDE, lambda x: np.abs(x).max())):
+    got = codec.client_norms(dev, kind).cpu().numpy()
+    np.testing.assert_allclose(got, [fn(x) for x in xs], rtol=1e-6)
