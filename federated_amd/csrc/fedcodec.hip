@@ -1749,6 +1749,10 @@ constexpr int kDecChunk = FC_DEC_CHUNK;  // 16-byte blocks per chunk (one 64-B l
 #ifndef FC_DEC_LONG
 #define FC_DEC_LONG 4
 #endif
+#ifndef FC_DEC_STEPS
+#define FC_DEC_STEPS 2
+#endif
+constexpr int kDecSteps = FC_DEC_STEPS;  // table steps per iteration (2 always fit the window)
 constexpr int kDecLong = FC_DEC_LONG;  // iterations between arithmetic-decode slots (power of 2)
 struct SegReader {
   const uint4* p;
@@ -1895,14 +1899,16 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     if ((++it & (kDecBatch - 1)) == 0) r.batch();  // every active lane is on the same iteration
     uint32_t moved = 0;
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {  // two table steps (the window holds >= 33 bits)
+    for (int st = 0; st < kDecSteps; ++st) {  // table steps (the window holds >= 32 bits)
 #if FC_DEC_ABL & 4  // diagnostics: conflict-free table reads (every lane its own bank; wrong codes)
       uint32_t e = lut[((uint32_t)(r.win >> 58) << 6) | (threadIdx.x & 63u)];
 #else
       uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
 #endif
       // codes past the segment end belong to the client's next tile: such an entry is dropped
-      e = (e >> 26) <= (uint32_t)(total - cons) ? e : 0u;
+      // (from the third step on, so is one reaching past the window's valid bits)
+      const int32_t lim = st < 2 ? total - cons : min(total - cons, fill - cons);
+      e = (e >> 26) <= (uint32_t)lim ? e : 0u;
       relb += e & 0x7Fu;
       acc_add_at<FACC>(relb, ((int32_t)(e << 12)) >> 26, scale);
       relb += (e >> 7) & 0x7Fu;
