@@ -44,7 +44,10 @@ constexpr int kTE = FC_TILE_ELEMS;  // elements per tile
 constexpr int kThreads = 256;       // 4 waves of 64 (decoder and small kernels)
 constexpr int kEncThreads = 64;     // encoder workgroup = one wavefront = one tile at a time
 constexpr int kChunks = kTE / (4 * kEncThreads);  // 4 chunks of 4 elements per lane
-constexpr int kWinWords = 544;      // per-wave LDS bit window (17 Kbit, ~16.9 bits/element)
+#ifndef FC_WIN_WORDS
+#define FC_WIN_WORDS 544
+#endif
+constexpr int kWinWords = FC_WIN_WORDS;  // per-wave LDS bit window (17 Kbit, ~16.9 bits/element)
 constexpr uint32_t kNoPos = 0x1FFF; // "no nonzero" in a 13-bit tile-relative field
 // Ticket streams: one device-scope atomic word saturates near 90 dequeues/us
 // (MI355X_MICROARCH.md "dequeue"), so tickets come from kTicketShards counters,
