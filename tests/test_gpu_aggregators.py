@@ -313,7 +313,7 @@ def test_drive_matches_oracle(gpu, scaling):
   np.testing.assert_allclose(out.measurements["avg_distortion"], m["avg_distortion"], rtol=1e-5)
 
 
-@pytest.mark.parametrize("P", [1, 3, 4096, 5000, 1 << 17, 300001])
+@pytest.mark.parametrize("P", [1, 3, 4096, 5000, 1 << 17, 300001, (1 << 21) + 5])  # last: 3 passes
 def test_hadamard_matches_oracle_and_round_trips(gpu, P):
   rng = np.random.default_rng(P)
   x = rng.standard_normal(P).astype(np.float32)
