@@ -203,3 +203,15 @@ def test_decode_tile_ranges_match_full_decode(gpu):
     assert (pout[hi:].cpu().numpy() == -7.0).all()
   np.testing.assert_array_equal(pout.cpu().numpy(), fout.cpu().numpy())
   assert int(err.item()) == 0
+
+
+def test_noise_sum_many_clients(gpu):
+  """fc_noise_sum with more clients than one 256-client key chunk: the client-order
+  float32 sum of TF's dither noise, bit-exact against the oracle."""
+  P, C = 1001, 300
+  seeds = np.array([[3 * c + 1, 7 * c + 2] for c in range(C)], np.int64)
+  want = np.zeros(P, np.float32)
+  for c in range(C):
+    want = want + oq.generate_noise(tuple(seeds[c]), P)
+  got = codec.noise_sum(torch.from_numpy(seeds), P, gpu).cpu().numpy()
+  np.testing.assert_array_equal(got, want)
