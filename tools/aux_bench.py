@@ -1,7 +1,7 @@
 """Diagnostic: time the auxiliary kernels of the §8 rows at bench-like sizes.
 
 client norms (QSGD / wrappers), dithered noise sum, step-size vote lengths,
-Hadamard rotation.  Prints ms and the fp32-read rate of each.
+elementwise quantise / dequantise, Hadamard rotation.  Prints ms and the fp32-read rate of each.
 """
 import os
 import sys
@@ -40,5 +40,9 @@ timed("noise_sum dithered (C x 25M)", lambda: codec.noise_sum(seeds, P, dev), P 
 timed("vote_lengths K=4 (64 x 25M)",
       lambda: codec.vote_lengths(rows[:64], np.array([0.25, 0.5, 1.0, 2.0], np.float32), seeds[:64],
                                  _lib.STOCHASTIC), 64 * P * 4, reps=1)
+big = torch.randn(1 << 25, generator=g, device=dev)  # 128 MiB (P limit 2^26 - 1)
+timed("quantize stochastic (2^25, q out)", lambda: codec.quantize(big, 0.5, (1, 2), _lib.STOCHASTIC), (1 << 25) * 8)
+timed("dequantize (2^25)", lambda: codec.dequantize(big.view(torch.int32), 0.5), (1 << 25) * 8)
+del big
 H = [torch.randn(1 << 24, generator=g, device=dev) for _ in range(64)]
 timed("hadamard 64 x 2^24 (fwd)", lambda: codec.hadamard_(H, (1, 2)), 64 * (1 << 24) * 4 * 2)
