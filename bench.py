@@ -16,9 +16,23 @@ on device, and resident in HBM before the timed region starts; the delta pool
 (by default a distinct 100 MB delta per client, 102 GB at C = 1024) is far
 beyond the 256 MiB Infinity Cache, so every client streams from HBM.
 
+At N = 1 the same JSON line also carries ``workloads``: one object per other
+single-GPU workload BASELINE.json / BASELINE.md name, each with its own
+HIP-event kernel timings and roofline (dominant kernel's algorithmic bytes per
+launch / its launch time vs the 8 TB/s HBM peak):
+  headline_uniform  the trainer's default rounding (trainer.py:63-65) on the headline round
+  trainer_round     the trainer-default builder round at 1024 x 25 M: fused
+                    L2 + Linf wrapper-norm pass, clip x weight pre-scale fused
+                    into the encoder, decode, weighted mean (builder.py:77-117)
+  config2           128 x 2^20, stochastic step 1/127, sigma 0.25 ("8-bit")
+  config3           256 x 4,050,748 (StackOverflow LSTM), stochastic step 1.0
+  onebit            config 5's codec: 1024 x 25 M one-bit SGD (one_bit_sgd.py:45-112)
+  copy              a 16-byte-per-lane HBM copy (the achievable streaming rate)
+``--workload NAME`` runs one of them alone (for rocprofv3 passes of one workload).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--clients C]
        [--mode stochastic|uniform|dithered] [--no-cpu-baseline] [--slabs S]
-       [--dump-result PATH]
+       [--workload all|headline|NAME] [--dump-result PATH]
 
 N > 1: each rank decodes its clients in S tile ranges and all-reduces each range
 while the next decodes.  Rehearsal on a 1-GPU box (never used by the driver):
@@ -42,6 +56,7 @@ from federated_amd import codec  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 MODES = {"uniform": _lib.UNIFORM, "stochastic": _lib.STOCHASTIC, "dithered": _lib.DITHERED}
+EXTRA = ["headline_uniform", "trainer_round", "config2", "config3", "onebit", "copy"]
 
 
 def parse():
@@ -63,6 +78,10 @@ def parse():
                   help="rank 0 saves the round's dequantised sum (.npy) to compare world sizes")
   ap.add_argument("--slabs", type=int, default=4,
                   help="N > 1: tile ranges decoded in turn, each all-reduced while the next decodes")
+  ap.add_argument("--workload", default="all", choices=["all", "headline"] + EXTRA,
+                  help="all (N=1 default): headline line + every extra workload; headline: the "
+                       "headline only; NAME: that workload alone (profiling)")
+  ap.add_argument("--extra-steps", type=int, default=5, help="timed steps per extra workload")
   return ap.parse_args()
 
 
@@ -125,57 +144,266 @@ def cpu_baseline(args):
                         n, P, args.mode, args.step_size, cores, t)}
 
 
-def measured_traffic(args, C):
-  """Per-launch HBM bytes of k_encode from the latest committed PMC profile of this exact
-  workload (profiles/*/traffic.json, written from tools/profile_bench.sh's FETCH_SIZE and
-  WRITE_SIZE passes with the gfx950 correction), else None."""
+def measured_traffic(workload, kernel):
+  """Per-launch HBM bytes of `kernel` in `workload` from the latest committed PMC
+  profile (profiles/*/traffic_<workload>.json, written by tools/make_profile_record.py
+  from separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 correction), else None."""
   import glob  # pylint: disable=g-import-not-at-top
   best = None
-  for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
+  for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_%s.json" % workload))):
     try:
       with open(f) as fh:
         d = json.load(fh)
     except (OSError, ValueError):
       continue
-    cfg = d.get("config", {})
-    if (cfg.get("clients"), cfg.get("P"), cfg.get("mode"), cfg.get("step")) == (C, args.P, args.mode,
-                                                                               args.step_size):
+    if kernel in d:
       best = (f, d)
   if best is None:
     return None, None
-  return best[1]["k_encode"]["hbm_bytes_corrected"], os.path.relpath(best[0], ROOT)
+  return best[1][kernel]["hbm_bytes_corrected"], os.path.relpath(best[0], ROOT)
+
+
+class Timer:
+  """HIP events around named phases on one stream (the stream the kernels run on)."""
+
+  def __init__(self, stream):
+    self.stream = stream
+    self.acc = {}
+    self.n = {}
+
+  def phase(self, name, fn):
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(self.stream)
+    r = fn()
+    e1.record(self.stream)
+    self.acc.setdefault(name, []).append((e0, e1))
+    return r
+
+  def ms(self):
+    torch.cuda.synchronize()
+    return {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in self.acc.items()}
+
+
+def roofline(kernel, alg_bytes, launch_ms, workload):
+  traffic, src = measured_traffic(workload, kernel)
+  return {"bound": "hbm", "kernel": kernel, "achieved": round(alg_bytes / launch_ms / 1e6, 1),
+          "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(alg_bytes / launch_ms / 1e-3 / HBM_PEAK, 4),
+          "traffic": round(traffic) if traffic else None, "traffic_source": src,
+          "alg_bytes_per_launch": alg_bytes, "launch_ms": round(launch_ms, 3)}
+
+
+def make_deltas(C, P, sigma, dev, seed0):
+  g = torch.Generator(device=dev)
+  rows = []
+  for i in range(C):
+    g.manual_seed(seed0 + i)
+    rows.append(torch.randn(P, generator=g, device=dev, dtype=torch.float32).mul_(sigma))
+  return rows
+
+
+def codec_round(name, rows, ptrs, P, step, mode, steps, warmup, stream, cap_per_elem=1.0, workload=None):
+  """Encode + decode + dequantise rounds of one codec configuration; HIP-event timed."""
+  C = len(rows)
+  dev = rows[0].device
+  seeds = torch.tensor([[500 + c, 500 + c] for c in range(C)], dtype=torch.int64, device=dev)
+  cap = codec._round_up(int(P * cap_per_elem) + 256, 64)  # pylint: disable=protected-access
+  batch = codec.EncodedBatch(P, C, [cap] * C, dev)
+  out = torch.empty(P, dtype=torch.float32, device=dev)
+  err = torch.zeros(1, dtype=torch.int32, device=dev)
+  tm = Timer(stream)
+  for i in range(warmup + steps):
+    t = tm if i >= warmup else Timer(stream)
+    t.phase("k_encode", lambda: codec.quantize_encode(None, step, seeds, mode, ptrs=ptrs, P=P, out=batch,
+                                                      stream=stream))
+    t.phase("k_decode", lambda: codec.decode_accumulate(batch, want_sum=False, out=out, step=step, err=err,
+                                                        stream=stream))
+  ms = tm.ms()
+  if len(codec.check_overflow(batch)) or int(err.item()):
+    raise SystemExit("%s: overflow or malformed stream" % name)
+  S = float(batch.nbytes().astype(np.float64).sum())
+  t_step = ms["k_encode"] + ms["k_decode"]
+  return {
+      "workload": name, "clients": C, "P": P, "mode": [k for k, v in MODES.items() if v == mode][0],
+      "step_size": step, "ms_per_step": round(t_step, 3),
+      "value_GiBps": round(C * P * 4.0 / (t_step * 1e-3) / 2**30, 2),
+      "bits_per_element": round(8 * S / (C * P), 4),
+      "roofline": roofline("k_encode", C * 4.0 * P + S, ms["k_encode"], workload or name),
+      "decode": {"kernel": "k_decode", "launch_ms": round(ms["k_decode"], 3),
+                 "alg_GBps": round((S + 4.0 * P) / (ms["k_decode"] * 1e-3) / 1e9, 1)},
+      "step_roofline_frac": round((C * 4.0 * P + 2 * S + 12.0 * P) / (t_step * 1e-3) / HBM_PEAK, 4),
+  }
+
+
+def w_trainer_round(rows, ptrs, P, steps, warmup, stream):
+  """Trainer-default builder round (uniform, step 0.5, clipping + zeroing, weighted),
+  device part as builder.WrappedAggregationFactory runs it: ONE fused L2 + Linf norm
+  pass, host scalars for the wrapper scales (one 8-KB D2H), the clip scale x weight
+  pre-scale fused into the encoder, decode + dequantise, divide by the weight sum."""
+  C = len(rows)
+  dev = rows[0].device
+  step = 0.5
+  w = torch.arange(200, 200 + C, dtype=torch.float32)  # example counts
+  seeds = torch.tensor([[9 + c, 9 + c] for c in range(C)], dtype=torch.int64, device=dev)
+  cap = codec._round_up(P + 256, 64)  # pylint: disable=protected-access
+  batch = codec.EncodedBatch(P, C, [cap] * C, dev)
+  out = torch.empty(P, dtype=torch.float32, device=dev)
+  err = torch.zeros(1, dtype=torch.int32, device=dev)
+  denom = torch.full((1,), float(w.sum()), dtype=torch.float32, device=dev)
+  norms = torch.empty(2 * C, dtype=torch.float32, device=dev)
+  clip, zero_thr = np.float32(1.0), np.float32(21.0)
+
+  def norm_pass():
+    _lib.call("fc_client_norms_scaled", _lib.ptr(ptrs), C, P, _lib.NORM_L2_LINF, None, _lib.ptr(norms),
+              _lib.stream_handle(stream))
+
+  tm = Timer(stream)
+  t_wall = []
+  for i in range(warmup + steps):
+    t = tm if i >= warmup else Timer(stream)
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    t.phase("k_client_norms", norm_pass)
+    nh = norms.cpu().numpy().reshape(2, C)  # the wrapper scales are host scalars (sync)
+    l2, linf = nh[0], nh[1]
+    keep = ~(linf > zero_thr)
+    l2 = np.where(keep, l2, np.float32(0.0)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+      inv = np.where(l2 > 0, np.float32(1.0) / l2, np.float32(np.inf)).astype(np.float32)
+    s0 = np.where(keep, clip * np.minimum(inv, np.float32(1.0) / clip), np.float32(0.0)).astype(np.float32)
+    pre = torch.from_numpy(np.stack([s0, w.numpy()], 1).astype(np.float32)).to(dev, non_blocking=True)
+    t.phase("k_encode", lambda: codec.quantize_encode(None, step, seeds, _lib.UNIFORM, ptrs=ptrs, P=P, out=batch,
+                                                      stream=stream, prescale=pre))
+    t.phase("k_decode", lambda: codec.decode_accumulate(batch, want_sum=False, out=out, step=step, err=err,
+                                                        stream=stream))
+    t.phase("mean", lambda: out.div_(denom))
+    torch.cuda.synchronize()
+    if i >= warmup:
+      t_wall.append(time.perf_counter() - w0)
+  ms = tm.ms()
+  if len(codec.check_overflow(batch)) or int(err.item()):
+    raise SystemExit("trainer_round: overflow or malformed stream")
+  S = float(batch.nbytes().astype(np.float64).sum())
+  t_round = float(np.mean(t_wall)) * 1e3
+  return {
+      "workload": "trainer_round", "clients": C, "P": P, "mode": "uniform", "step_size": step,
+      "clipping": True, "zeroing": True, "weighted": True,
+      "ms_per_step": round(t_round, 3), "value_GiBps": round(C * P * 4.0 / (t_round * 1e-3) / 2**30, 2),
+      "kernels_ms": {k: round(v, 3) for k, v in ms.items()},
+      "bits_per_element": round(8 * S / (C * P), 4),
+      "roofline": roofline("k_encode", C * 4.0 * P + S, ms["k_encode"], "trainer_round"),
+      "norms_roofline": roofline("k_client_norms", C * 4.0 * P, ms["k_client_norms"], "trainer_round"),
+  }
+
+
+def w_onebit(rows, ptrs, P, steps, warmup, stream):
+  """Config 5's codec on one GPU: 1024 x 25 M one-bit SGD encode + client-order decode-sum."""
+  C = len(rows)
+  dev = rows[0].device
+  nw = (P + 31) // 32
+  masks = torch.empty(C * nw, dtype=torch.int32, device=dev)
+  means = torch.empty(2 * C, dtype=torch.float32, device=dev)
+  dist = torch.empty(C, dtype=torch.float64, device=dev)
+  out = torch.empty(P, dtype=torch.float32, device=dev)
+  h = _lib.stream_handle(stream)
+  tm = Timer(stream)
+  for i in range(warmup + steps):
+    t = tm if i >= warmup else Timer(stream)
+    t.phase("k_mask_encode", lambda: _lib.call("fc_onebit_encode", _lib.ptr(ptrs), C, P, 0.0, _lib.ptr(masks),
+                                                _lib.ptr(means), _lib.ptr(dist), h))
+    t.phase("k_onebit_decode_sum", lambda: _lib.call("fc_onebit_decode_sum", _lib.ptr(masks), _lib.ptr(means), C,
+                                                      P, _lib.ptr(out), h))
+  ms = tm.ms()
+  t_step = ms["k_mask_encode"] + ms["k_onebit_decode_sum"]
+  enc_bytes = C * 4.0 * P + C * 4.0 * nw
+  return {
+      "workload": "onebit", "clients": C, "P": P, "codec": "one-bit SGD, threshold 0",
+      "ms_per_step": round(t_step, 3), "value_GiBps": round(C * P * 4.0 / (t_step * 1e-3) / 2**30, 2),
+      "roofline": roofline("k_mask_encode", enc_bytes, ms["k_mask_encode"], "onebit"),
+      "decode": {"kernel": "k_onebit_decode_sum", "launch_ms": round(ms["k_onebit_decode_sum"], 3),
+                 "alg_GBps": round((C * 4.0 * nw + 4.0 * P) / (ms["k_onebit_decode_sum"] * 1e-3) / 1e9, 1)},
+  }
+
+
+def w_copy(dev, stream, steps=10):
+  n = 4 << 30
+  a = torch.empty(n, dtype=torch.uint8, device=dev)
+  b = torch.empty(n, dtype=torch.uint8, device=dev)
+  a.fill_(1)
+  h = _lib.stream_handle(stream)
+  tm = Timer(stream)
+  for i in range(2 + steps):
+    t = tm if i >= 2 else Timer(stream)
+    t.phase("k_copy_f4", lambda: _lib.call("fc_copy", _lib.ptr(b), _lib.ptr(a), n, h))
+  ms = tm.ms()["k_copy_f4"]
+  gbps = 2.0 * n / (ms * 1e-3) / 1e9
+  del a, b
+  return {"workload": "copy", "bytes_moved_per_launch": 2 * n, "launch_ms": round(ms, 3),
+          "achieved_GBps": round(gbps, 1), "frac_of_8TBps": round(gbps * 1e9 / HBM_PEAK, 4)}
+
+
+def run_extra(name, args, dev, stream, head_rows, head_ptrs):
+  steps, warmup = args.extra_steps, 2
+  P = args.P
+  if name == "headline_uniform":
+    return codec_round(name, head_rows, head_ptrs, P, 0.5, _lib.UNIFORM, steps, warmup, stream)
+  if name == "trainer_round":
+    return w_trainer_round(head_rows, head_ptrs, P, steps, warmup, stream)
+  if name == "onebit":
+    return w_onebit(head_rows, head_ptrs, P, steps, warmup, stream)
+  if name == "copy":
+    return w_copy(dev, stream)
+  if name == "config2":
+    rows = make_deltas(128, 1 << 20, 0.25, dev, 7000)
+    step = 1.0 / 127
+  else:  # config3
+    rows = make_deltas(256, 4_050_748, 1.0, dev, 9000)
+    step = 1.0
+  ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+  r = codec_round(name, rows, ptrs, rows[0].numel(), step, _lib.STOCHASTIC, max(steps, 10), warmup, stream,
+                  cap_per_elem=2.5 if name == "config2" else 1.0)
+  del rows
+  return r
 
 
 def main():
   args = parse()
   rank, world = setup_dist(args)
   dev = torch.device("cuda", torch.cuda.current_device())
+  stream = torch.cuda.current_stream()
   P = args.P
   C = args.clients
   assert C % world == 0, "clients must divide evenly over ranks"
   Cg = C // world
   mode = MODES[args.mode]
+  single = args.workload not in ("all", "headline")
 
   # ---- synthetic inputs, resident in HBM before timing ----
   g = torch.Generator(device=dev)
   g.manual_seed(20251015 + rank)
   npool = args.pool if args.pool > 0 else Cg
   pool = []
-  for i in range(npool):
+  need_head = not single or args.workload in ("headline_uniform", "trainer_round", "onebit")
+  for i in range(npool if need_head else 0):
     if npool == Cg:  # a delta per client, seeded by its global index: any --gpus N sums the same round
       g.manual_seed(20251015 + rank * Cg + i)
     t = torch.randn(P, generator=g, device=dev, dtype=torch.float32)
     pool.append(t.mul_(args.sigma))
-  rows = [pool[c % npool] for c in range(Cg)]
-  ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+  rows = [pool[c % npool] for c in range(Cg)] if pool else []
+  ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev) if rows else None
+
+  if single:  # one extra workload alone (profiling runs)
+    r = run_extra(args.workload, args, dev, stream, rows, ptrs)
+    print(json.dumps(r), flush=True)
+    return r
+
   base = 1000 + rank * Cg
   seeds = torch.tensor([[base + c, base + c] for c in range(Cg)], dtype=torch.int64, device=dev)
-  cap = codec._round_up(int(P * args.cap_bytes_per_elem) + 256, 64)
+  cap = codec._round_up(int(P * args.cap_bytes_per_elem) + 256, 64)  # pylint: disable=protected-access
   batch = codec.EncodedBatch(P, Cg, [cap] * Cg, dev)
   out = torch.empty(P, dtype=torch.float32, device=dev)
   isum = torch.empty(P, dtype=torch.int32, device=dev)
   err = torch.zeros(1, dtype=torch.int32, device=dev)
-  stream = torch.cuda.current_stream()
   if world > 1:
     import torch.distributed as dist  # pylint: disable=g-import-not-at-top
 
@@ -239,28 +467,24 @@ def main():
   # ---- per-kernel timing of the dominant kernel (HIP events on its stream) ----
   nbytes = batch.nbytes().astype(np.float64)
   S = float(nbytes.sum())
-  e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+  tm = Timer(stream)
   reps = max(2, min(args.steps, 5))
-  t_enc = t_dec = 0.0
   for _ in range(reps):
-    e[0].record(stream)
-    codec.quantize_encode(None, args.step_size, seeds, mode, ptrs=ptrs, P=P, out=batch, stream=stream)
-    e[1].record(stream)
-    codec.decode_accumulate(batch, want_sum=False, out=out, step=args.step_size, err=err, stream=stream)
-    e[2].record(stream)
-    torch.cuda.synchronize()
-    t_enc += e[0].elapsed_time(e[1]) / 1e3
-    t_dec += e[1].elapsed_time(e[2]) / 1e3
-  t_enc /= reps
-  t_dec /= reps
+    tm.phase("k_encode", lambda: codec.quantize_encode(None, args.step_size, seeds, mode, ptrs=ptrs, P=P,
+                                                       out=batch, stream=stream))
+    tm.phase("k_decode", lambda: codec.decode_accumulate(batch, want_sum=False, out=out, step=args.step_size,
+                                                         err=err, stream=stream))
+  ms = tm.ms()
   enc_bytes = Cg * 4.0 * P + S  # fp32 read + code write
   dec_bytes = S + 4.0 * P  # code read + f32 result write
   step_bytes = Cg * 4.0 * P + 2 * S + 12.0 * P  # BASELINE.md B_alg per GPU
 
   result = None
-  traffic, traffic_src = measured_traffic(args, C) if world == 1 else (None, None)
   if rank == 0:
     value = C * P * 4.0 / t_step / 2**30
+    headline_name = "headline" if (args.mode, args.step_size, C, P) == ("stochastic", 0.5, 1024, 25_000_000) \
+        else "custom"
+    rl = roofline("k_encode", enc_bytes, ms["k_encode"], headline_name if world == 1 else "none")
     result = {
         "metric": "device-resident encode+decode GiB/s on 25M-fp32 deltas",
         "value": round(value, 3),
@@ -281,20 +505,22 @@ def main():
                                                                                  args.step_size),
                    "clients_per_gpu": Cg, "parallelism": "client-sharded dp%d + RCCL int32 all-reduce"
                    % world if world > 1 else "1 GPU"},
-        "roofline": {"bound": "hbm", "kernel": "k_encode",
-                     "achieved": round(enc_bytes / t_enc / 1e9, 1),
-                     "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                     "frac": round(enc_bytes / t_enc / HBM_PEAK, 4),
-                     "traffic": round(traffic) if traffic else None,
-                     "traffic_source": traffic_src,
-                     "alg_bytes_per_launch": enc_bytes, "launch_ms": round(t_enc * 1e3, 3)},
-        "decode": {"kernel": "k_decode", "launch_ms": round(t_dec * 1e3, 3),
-                   "alg_GBps": round(dec_bytes / t_dec / 1e9, 1)},
+        "roofline": rl,
+        "decode": {"kernel": "k_decode", "launch_ms": round(ms["k_decode"], 3),
+                   "alg_GBps": round(dec_bytes / (ms["k_decode"] * 1e-3) / 1e9, 1)},
         "step_roofline": {"alg_bytes_per_gpu": step_bytes,
                           "achieved_GBps": round(step_bytes / t_step / 1e9, 1),
                           "frac": round(step_bytes / t_step / HBM_PEAK, 4)},
         "bits_per_element": round(8 * S / (Cg * P), 4),
     }
+  if world == 1 and args.workload == "all":
+    extras = {}
+    for name in EXTRA:
+      torch.cuda.synchronize()
+      extras[name] = run_extra(name, args, dev, stream, rows, ptrs)
+      torch.cuda.empty_cache()
+    result["workloads"] = extras
+  if rank == 0:
     if world == 1 and not args.no_cpu_baseline:
       result["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(result), flush=True)

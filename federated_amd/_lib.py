@@ -10,7 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDCODEC_LIB") or os.path.join(_HERE, "libfedcodec.so")
 
 UNIFORM, STOCHASTIC, DITHERED = 0, 1, 2
-NORM_MEAN_MAGNITUDE, NORM_MAX_MAGNITUDE, NORM_DIMENSIONLESS, NORM_L2, NORM_LINF = 1, 2, 3, 4, 5
+NORM_MEAN_MAGNITUDE, NORM_MAX_MAGNITUDE, NORM_DIMENSIONLESS, NORM_L2, NORM_LINF, NORM_L2_LINF = 1, 2, 3, 4, 5, 6
 TILE_ELEMS = 1024
 MAX_ELEMS = (1 << 26) - 1
 
@@ -36,8 +36,10 @@ SIGNATURES = {
     "fc_vote_workspace_bytes": (_I64, [_I32, _I64, _I32]),
     "fc_vote_lengths": (_INT, [_P, _I32, _I64, _P, _I32, _P, _INT, _P, _P, _P, _I64, _P]),
     "fc_dequantize": (_INT, [_P, _I64, _F32, _P, _P, _P]),
+    "fc_copy": (_INT, [_P, _P, _I64, _P]),
     "fc_noise_sum": (_INT, [_P, _I32, _I64, _P, _P]),
     "fc_client_norms": (_INT, [_P, _I32, _I64, _INT, _P, _P]),
+    "fc_client_norms_scaled": (_INT, [_P, _I32, _I64, _INT, _P, _P, _P]),
     "fc_finalize": (_INT, [_P, _P, _I32, _I64, _P, _P, _P]),
     "fc_onebit_encode": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _P]),
     "fc_drive_encode": (_INT, [_P, _I32, _I64, _INT, _P, _P, _P, _P]),

@@ -117,9 +117,12 @@ class QuantizeEncodeFactory(tc.UnweightedAggregationFactory):
       if seeds is None:
         seeds = clock_seeds(C)
       seeds = torch.as_tensor(np.asarray(seeds, np.int64).reshape(C, 2)).cuda()
-      norms = codec.client_norms(rows, factory._norm_kind) if factory._norm_kind else None
       if prescale is not None:  # fused TFF wrapper scales (builder.configure_aggregator)
         prescale = torch.as_tensor(np.asarray(prescale, np.float32).reshape(C, 2)).cuda()
+      # normalize_fn sees the value behind the clipping / mean wrappers (:145): the
+      # norm of the pre-scaled elements, as the encoder quantises them
+      norms = (codec.client_norms(rows, factory._norm_kind, prescale=prescale)
+               if factory._norm_kind else None)
       batch = codec.quantize_encode_checked(rows, step_size, seeds, factory._mode, norms=norms,
                                             prescale=prescale)
       noise_sum = codec.noise_sum(seeds, P, rows[0].device) if factory._mode == _lib.DITHERED else None

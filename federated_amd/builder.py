@@ -123,7 +123,17 @@ class HadamardTransformFactory(tc.UnweightedAggregationFactory):
 
 
 class QuantileEstimate:
-  """``PrivateQuantileEstimationProcess.no_noise`` (geometric update) restated."""
+  """``PrivateQuantileEstimationProcess.no_noise`` (geometric update) restated.
+
+  The process keeps a raw estimate X.  ``report()`` is the affine map
+  multiplier * X + increment that TFF applies to the reported value only
+  (``EstimationProcess.map``); the quantile query itself records, per client,
+  whether the client's norm is <= the RAW estimate X (tensorflow_privacy
+  ``QuantileEstimatorQuery``), and moves X geometrically:
+  X <- X * exp(-lr * (frac_below - target_quantile)).  For zeroing (2X + 1,
+  q = 0.98) X therefore tracks the 98th percentile of the client norms and the
+  zeroing threshold sits at about twice it.
+  """
 
   def __init__(self, initial_estimate, target_quantile, learning_rate, multiplier=1.0,
                increment=0.0):
@@ -137,8 +147,7 @@ class QuantileEstimate:
     return F32(estimate * self.multiplier + self.increment)
 
   def update(self, estimate, norms):
-    thr = self.report(estimate)
-    below = F32(np.mean((np.asarray(norms, np.float32) <= thr).astype(np.float32)))
+    below = F32(np.mean((np.asarray(norms, np.float32) <= F32(estimate)).astype(np.float32)))
     return F32(estimate * np.exp(-self.learning_rate * (below - self.target_quantile)))
 
 
@@ -189,13 +198,14 @@ class WrappedAggregationFactory(tc.WeightedAggregationFactory):
            else np.ones(C, np.float32))
       s0 = np.ones(C, np.float32)
       zero_norm = clip_norm = ()
+      if wrap._zero or wrap._clip:
+        # both wrapper norms from ONE read pass over the round's deltas
+        l2, linf = codec.client_norms(rows, _lib.NORM_L2_LINF).cpu().numpy()
       if wrap._zero:
-        linf = codec.client_norms(rows, _lib.NORM_LINF).cpu().numpy()
         zero_norm = wrap._zero.report(state["zeroing_norm"])
         keep = ~(linf > zero_norm)
         s0 = np.where(keep, s0, F32(0.0)).astype(np.float32)
       if wrap._clip:
-        l2 = codec.client_norms(rows, _lib.NORM_L2).cpu().numpy()
         l2 = np.where(s0 == 0, F32(0.0), l2).astype(np.float32)  # zeroed clients have norm 0
         clip_norm = wrap._clip.report(state["clipping_norm"])
         with np.errstate(divide="ignore"):
@@ -206,7 +216,10 @@ class WrappedAggregationFactory(tc.WeightedAggregationFactory):
       out = call_inner(inner, state["inner_state"], rows, seeds=seeds, prescale=prescale)
       denom = F32(np.sum(w, dtype=np.float32)) if wrap._weighted else F32(C)
       res = torch.as_tensor(out.result).cuda().reshape(-1)
-      res = res / denom if denom != 0 else torch.zeros_like(res)
+      # divide_no_nan: an IEEE float32 division by a device scalar (a Python-scalar
+      # divisor would be turned into a multiply by its reciprocal)
+      res = (res / torch.full((1,), float(denom), dtype=res.dtype, device=res.device)
+             if denom != 0 else torch.zeros_like(res))
       new_state = collections.OrderedDict(
           zeroing_norm=(wrap._zero.update(state["zeroing_norm"], linf) if wrap._zero else ()),
           clipping_norm=(wrap._clip.update(state["clipping_norm"], l2) if wrap._clip else ()),

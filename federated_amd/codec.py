@@ -136,15 +136,53 @@ def check_overflow(batch):
 
 
 def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None, prescale=None):
-  """quantize_encode, re-encoding with worst-case capacity if any client overflowed."""
+  """quantize_encode; clients whose code overflowed their capacity are re-encoded.
+
+  The encoder reports every client's exact bit length even on overflow, so only
+  the overflowed clients are encoded again, into exactly sized buffers, and the
+  batch is re-packed around them (the other clients' codes are copied, not
+  recomputed).  A client's code does not depend on the rest of its batch.
+  """
   rows = _rows(xs, torch.float32)
-  P = rows[0].numel()
   batch = quantize_encode(rows, step, seeds, mode, norms=norms, caps=caps, prescale=prescale)
-  if len(check_overflow(batch)):
-    batch = quantize_encode(rows, step, seeds, mode, norms=norms, prescale=prescale,
-                            caps=[worst_case_capacity(P)] * len(rows))
-    assert not len(check_overflow(batch))
-  return batch
+  bad = check_overflow(batch)
+  if not len(bad):
+    return batch
+  C = len(rows)
+  device = batch.device
+  sel = torch.as_tensor(bad, dtype=torch.int64, device=device)
+  seeds = torch.as_tensor(seeds, dtype=torch.int64).reshape(C, 2).to(device)
+  need = (batch.bits()[bad] + 7) // 8 + 256
+  sub = quantize_encode([rows[c] for c in bad], step, seeds[sel], mode,
+                        norms=None if norms is None else norms[sel], caps=list(need),
+                        prescale=None if prescale is None else
+                        torch.as_tensor(prescale).reshape(C, 2).to(device)[sel].contiguous())
+  assert not len(check_overflow(sub))
+  new_caps = batch.caps_host.copy()
+  new_caps[bad] = sub.caps_host
+  return _repack(batch, sub, bad, new_caps)
+
+
+def _repack(batch, sub, bad, caps):
+  """A batch with capacities `caps` holding batch's clients, except clients `bad`
+  (in order), which come from `sub`."""
+  out = EncodedBatch(batch.P, batch.nclients, list(caps), batch.device)
+  T1 = batch.T + 1
+  T = batch.T
+  src_of = {int(c): (sub, i) for i, c in enumerate(bad)}
+  nbytes = batch.nbytes()
+  sub_nbytes = sub.nbytes()
+  for c in range(batch.nclients):
+    b, i = src_of.get(c, (batch, c))
+    n = int(sub_nbytes[i] if b is sub else nbytes[c])
+    o_src, o_dst = int(b.offs_host[i]), int(out.offs_host[c])
+    out.stream[o_dst:o_dst + n].copy_(b.stream[o_src:o_src + n])
+    out.idx[c * T1:(c + 1) * T1].copy_(b.idx[i * T1:(i + 1) * T1])
+    out.total_bits[c:c + 1].copy_(b.total_bits[i:i + 1])
+    out.dist_part[c * T:(c + 1) * T].copy_(b.dist_part[i * T:(i + 1) * T])
+    out.nnz_part[c * T:(c + 1) * T].copy_(b.nnz_part[i * T:(i + 1) * T])
+  out.overflow.zero_()
+  return out
 
 
 def rlgamma_encode(qs, caps=None):
@@ -270,14 +308,24 @@ def noise_sum(seeds, P, device):
   return out
 
 
-def client_norms(xs, kind):
+def client_norms(xs, kind, prescale=None):
+  """Per-client norms (fc_client_norms_scaled), float32 on the device.
+
+  ``prescale``: optional device float32 [C, 2]; the norm is then of
+  (x * prescale[c, 0]) * prescale[c, 1] element by element.  ``kind`` NORM_L2_LINF
+  returns [2, C] (row 0 the L2 norms, row 1 max |x|) from one pass; else [C].
+  """
   rows = _rows(xs, torch.float32)
   P = rows[0].numel()
+  C = len(rows)
   ptrs = _ptr_array(rows, rows[0].device)
-  norms = torch.empty(len(rows), dtype=torch.float32, device=rows[0].device)
-  _lib.call("fc_client_norms", _lib.ptr(ptrs), len(rows), P, int(kind), _lib.ptr(norms),
-            _lib.stream_handle())
-  return norms
+  both = int(kind) == _lib.NORM_L2_LINF
+  norms = torch.empty((2 * C) if both else C, dtype=torch.float32, device=rows[0].device)
+  if prescale is not None:
+    prescale = torch.as_tensor(prescale, dtype=torch.float32).reshape(C, 2).to(rows[0].device).contiguous()
+  _lib.call("fc_client_norms_scaled", _lib.ptr(ptrs), C, P, int(kind), _lib.ptr(prescale),
+            _lib.ptr(norms), _lib.stream_handle())
+  return norms.reshape(2, C) if both else norms
 
 
 def onebit_encode(xs, threshold=0.0):

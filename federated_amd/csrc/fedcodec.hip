@@ -5,10 +5,10 @@
 //   k_encode  one pass over the fp32 client deltas: quantise (TF-CPU numerics,
 //             Philox4x32-10 stochastic rounding), per-element run-length Elias
 //             gamma code lengths, wavefront scans, single-pass decoupled
-//             look-back across 4096-element tiles, LDS-staged MSB-first bit
+//             look-back across 1024-element tiles, LDS-staged MSB-first bit
 //             packing, owner-writes-word stores (no memset, no global atomics on
 //             the stream), per-tile decoder index.
-//   k_decode  per 4096-element tile, one lane per client: sequential gamma
+//   k_decode  per 1024-element tile, one lane per client: sequential gamma
 //             decode of that client's tile segment from the encoder index,
 //             LDS int32 accumulation, fused dequantise epilogue.
 //
@@ -1657,7 +1657,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Decoder: one workgroup per (group of) 4096-element tile(s), one lane per client.
+// Decoder: one workgroup per (group of) 1024-element tile(s), one lane per client.
 // ---------------------------------------------------------------------------
 struct DecodeArgs {
   const uint8_t* stream_buf;
@@ -2108,17 +2108,28 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // Per-client normaliser / norm: one 1024-thread workgroup per client (enough
 // waves per CU even for a few hundred clients); each wave reads 2048-element
 // tiles with coalesced 4-byte loads, 8 in flight.  Max is exact in float32;
-// sums go through float32 per-lane tile partials (32 elements) into float64,
-// reduced in a fixed order.  Inputs pass through `+ 0.0f` (DAZ as TF-CPU).
+// sums accumulate every term in float64 (|x| and x^2 of a float32 are exact in
+// float64), reduced in a fixed order: the float32 result is the correctly
+// rounded norm but in astronomically rare ties.  The pass stays HBM-bound.
+// Inputs pass through `+ 0.0f` (DAZ as TF-CPU).
+// prescale (nullable [2C]): the norm of (x * prescale[2c]) * prescale[2c+1],
+// element by element as the encoder quantises it (the value QuantizeEncode's
+// normalize_fn sees behind the TFF clipping and mean wrappers).
+// FC_NORM_L2_LINF: one pass for both wrapper norms, norms[c] = ||x||_2 and
+// norms[C + c] = max |x| (builder.py:100-117: clipping and zeroing).
 constexpr int kNormThreads = 1024;
 __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* const* xs, int64_t P,
-                                                               int kind, float* norms) {
+                                                               int kind, const float* prescale,
+                                                               float* norms) {
   __shared__ double red[kNormThreads / 64];
+  __shared__ float redm[kNormThreads / 64];
   const int c = blockIdx.x;
   const float* __restrict__ x = xs[c];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool both = kind == FC_NORM_L2_LINF;
   const bool is_max = kind == FC_NORM_MAX_MAGNITUDE || kind == FC_NORM_LINF;
   const bool is_abs = kind == FC_NORM_MEAN_MAGNITUDE;
+  const float s0 = prescale ? prescale[2 * c] : 1.0f, s1 = prescale ? prescale[2 * c + 1] : 1.0f;
   const int64_t ntile = (P + 2047) / 2048;
   double acc = 0.0;
   float mx = 0.0f;
@@ -2126,7 +2137,6 @@ __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* cons
     const int64_t base = tile * 2048;
     const bool full = base + 2048 <= P;
     const float* __restrict__ xt = x + base + lane;
-    float part = 0.0f;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       float raw[8];
@@ -2137,28 +2147,40 @@ __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* cons
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float a = fabsf(raw[j] + 0.0f);
+        float v = raw[j] + 0.0f;
+        if (prescale) v = (v * s0) * s1;
+        const float a = fabsf(v);
         mx = fmaxf(mx, a);
-        part += is_abs ? a : a * a;
+        const double ad = (double)a;
+        acc += is_abs ? ad : ad * ad;
       }
     }
-    acc += (double)part;
   }
   double r = is_max ? (double)mx : acc;
+  float m = mx;
 #pragma unroll
-  for (int m = 32; m > 0; m >>= 1) {
-    const double o = shfl_xor_f64(r, m);
-    r = is_max ? fmax(r, o) : r + o;
+  for (int o = 32; o > 0; o >>= 1) {
+    const double v = shfl_xor_f64(r, o);
+    r = is_max ? fmax(r, v) : r + v;
+    m = fmaxf(m, __shfl_xor(m, o));
   }
-  if (lane == 0) red[wv] = r;
+  if (lane == 0) {
+    red[wv] = r;
+    redm[wv] = m;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = red[0];
-    for (int w = 1; w < kNormThreads / 64; ++w) t = is_max ? fmax(t, red[w]) : t + red[w];
+    float tm = redm[0];
+    for (int w = 1; w < kNormThreads / 64; ++w) {
+      t = is_max ? fmax(t, red[w]) : t + red[w];
+      tm = fmaxf(tm, redm[w]);
+    }
     if (kind == FC_NORM_MEAN_MAGNITUDE) t = t / (double)P;
     if (kind == FC_NORM_DIMENSIONLESS) t = sqrt(t / (double)P);
-    if (kind == FC_NORM_L2) t = sqrt(t);
+    if (kind == FC_NORM_L2 || both) t = sqrt(t);
     norms[c] = (float)t;
+    if (both) norms[gridDim.x + c] = tm;
   }
 }
 
@@ -2189,162 +2211,156 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const float* dist_part, c
   }
 }
 
-// One-bit SGD (one_bit_sgd.py:56-81).  One 256-thread workgroup per client;
-// each wave walks 2048-element tiles with fully coalesced 4-byte loads: lane l
-// reads element 64k + l of the tile (k = 0..31), so the ballot of (v >= thr) is
-// mask words 2k and 2k+1 directly (TF's mask_above_threshold, bit i of word w =
-// element 32w + i); lanes 2k / 2k+1 collect them by writelane and each tile
-// stores its 64 words in one coalesced store.  Pass 1 sums values above / all
-// (f32 per lane per tile, f64 beyond); the count above is the ballots'
-// popcount.  Pass 2 (after the means) re-reads the tensor for the distortion
-// sum of (v - decoded)^2, each term in float32 as TF computes it.  Reductions
-// are in a fixed order (deterministic).  Inputs pass through `+ 0.0f` so
-// denormals flush as on TF-CPU before the comparison.
+// One-bit SGD (one_bit_sgd.py:56-81) and DRIVE (drive.py:58-76): ONE read
+// pass per client.  One 256-thread workgroup per client; each wave walks
+// 2048-element tiles with 16-byte loads, 8 in flight (lane l of load k: elements
+// 256 k + 4 l .. +3).  A lane's four comparison bits form a nibble; three DPP
+// rounds gather 8 lanes' nibbles into TF's mask word (bit i of word w = element
+// 32 w + i), and the tile's 64 words go out through LDS as one coalesced 256-B
+// store.  The means need the per-side sums and the distortion
+// sum (x - decoded)^2 needs the means, so instead of a second pass the
+// distortion is expanded per side:
+//   sum_side (x - m)^2 = S2 - 2 m S1 + n m^2,  S1 = sum x, S2 = sum x^2,
+// with every term accumulated in float64 (x^2 of a float32 is exact in float64;
+// the expansion then cancels at the 1e-16 level, well inside the tolerance on
+// TF's own float32 reduction).  Reductions are in a fixed order (deterministic).
+// Inputs pass through `+ 0.0f` so denormals flush as on TF-CPU before the
+// comparison.  KIND 0: one-bit SGD (threshold thr, class means).  KIND 1: DRIVE
+// (mask = !(x < 0), scale from sum |x| and sum x^2, means -scale / +scale).
 constexpr int kObThreads = 256;
 constexpr int kObWaves = kObThreads / 64;
 
+__device__ __forceinline__ uint32_t dpp_row_shl(uint32_t x, int n) {
+  // lane l reads lane l + n of its 16-lane row (0 past the row end)
+  return n == 1 ? __builtin_amdgcn_update_dpp(0u, x, 0x101, 0xf, 0xf, false)
+       : n == 2 ? __builtin_amdgcn_update_dpp(0u, x, 0x102, 0xf, 0xf, false)
+                : __builtin_amdgcn_update_dpp(0u, x, 0x104, 0xf, 0xf, false);
+}
 
-// KIND 0: one-bit SGD (threshold thr, class means).  KIND 1: DRIVE
-// (drive.py:58-76: mask = !(x < 0), scale from sum |x| and sum x^2, means
-// -scale / +scale); the same two passes, only the sums and the means differ.
 template <int KIND>
 __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* xs, int64_t P, float thr,
                                                             int min_distortion, uint32_t* masks,
                                                             float* means, double* dist) {
-  __shared__ double red[3][kObWaves];
+  __shared__ double red[4][kObWaves];
   __shared__ uint64_t redn[kObWaves];
-  __shared__ float mean_s[2];
+  __shared__ uint32_t wordbuf[kObWaves][64];
   const int c = blockIdx.x;
   const float* __restrict__ x = xs[c];
   const int64_t nw = (P + 31) / 32;
   uint32_t* __restrict__ m = masks + (int64_t)c * nw;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t ntile = (P + 2047) / 2048;
-  double sa = 0.0, st = 0.0;
-  uint64_t na = 0;
+  const bool aligned = ((uintptr_t)x & 15u) == 0;
+  // KIND 0: s1 = sum x, s2 = sum x^2, a1 / a2 = the same over x >= thr;
+  // KIND 1: s1 = sum |x|, s2 = sum x^2
+  double s1 = 0.0, s2 = 0.0, a1 = 0.0, a2 = 0.0;
+  uint32_t na = 0;
   // clients start at different tiles: rows share their alignment, and reading
   // every client's same offset at once would load the same HBM channels
   const int64_t t0 = ((int64_t)c * 977) % ntile;
   for (int64_t tt = wv; tt < ntile; tt += kObWaves) {
     const int64_t tile = tt + t0 < ntile ? tt + t0 : tt + t0 - ntile;
     const int64_t base = tile * 2048;
-    const bool full = base + 2048 <= P;
-    const float* __restrict__ xt = x + base + lane;
-    float fa = 0.0f, ft = 0.0f;
-    uint32_t word = 0;
+    const bool full = base + 2048 <= P && aligned;
+    float4 raw[8];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {  // 8 loads in flight, then their 8 ballots
-      float raw[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * g + j;
-        raw[j] = (full || base + 64 * k + lane < P) ? xt[64 * k] : 0.0f;
-      }
-      uint64_t bal[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * g + j;
-        const bool in = full || base + 64 * k + lane < P;
-        const float v = raw[j] + 0.0f;
-        const bool ab = in && !(v < thr);
-        bal[j] = __ballot(ab);
-        na += (uint64_t)__popcll(bal[j]);
-        if (KIND == 0) {  // sum above threshold, sum of all
-          ft += v;
-          fa += ab ? v : 0.0f;
-        } else {  // sum |x|, sum x^2
-          fa += fabsf(v);
-          ft += v * v;
-        }
-      }
-      // mask words 16g .. 16g+15 into lanes 16g .. 16g+15.  The ballots' SGPRs were
-      // written by VALU compares: wait states before each v_writelane pair reads one
-      // (the compiler does not pad inline asm, and may place a compare right before)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * g + j;
-        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2\n\tv_writelane_b32 %0, %3, %4"
-                     : "+v"(word)
-                     : "s"((uint32_t)bal[j]), "n"(2 * k), "s"((uint32_t)(bal[j] >> 32)), "n"(2 * k + 1));
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = base + 256 * k + 4 * lane;
+      if (full) {
+        raw[k] = *(const float4*)(x + e);
+      } else {
+        raw[k].x = e < P ? x[e] : 0.0f;
+        raw[k].y = e + 1 < P ? x[e + 1] : 0.0f;
+        raw[k].z = e + 2 < P ? x[e + 2] : 0.0f;
+        raw[k].w = e + 3 < P ? x[e + 3] : 0.0f;
       }
     }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = base + 256 * k + 4 * lane;
+      const float v4[4] = {raw[k].x + 0.0f, raw[k].y + 0.0f, raw[k].z + 0.0f, raw[k].w + 0.0f};
+      uint32_t nib = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool in = full || e + i < P;
+        const float v = v4[i];
+        const bool ab = in && !(v < thr);
+        nib |= ab ? (1u << i) : 0u;
+        const double vd = in ? (double)v : 0.0;
+        if (KIND == 0) {
+          s1 += vd;
+          s2 = fma(vd, vd, s2);
+          const double t = ab ? vd : 0.0;
+          a1 += t;
+          a2 = fma(t, t, a2);
+        } else {
+          s1 += fabs(vd);
+          s2 = fma(vd, vd, s2);
+        }
+      }
+      na += (uint32_t)__popc(nib);
+      // 8 lanes' nibbles -> one mask word in lane 8j (word 8k + j of the tile)
+      uint32_t wd = nib | (dpp_row_shl(nib, 1) << 4);
+      wd |= dpp_row_shl(wd, 2) << 8;
+      wd |= dpp_row_shl(wd, 4) << 16;
+      if ((lane & 7) == 0) wordbuf[wv][8 * k + (lane >> 3)] = wd;
+    }
+    __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses execute in order
+    const uint32_t word = wordbuf[wv][lane];
     if (tile * 64 + lane < nw) m[tile * 64 + lane] = word;
-    sa += (double)fa;
-    st += (double)ft;
   }
-  sa = wave_sum_f64(sa);
-  st = wave_sum_f64(st);
+  // fixed-order reductions: lanes (DPP/shuffle tree), then waves in order
+  s1 = wave_sum_f64(s1);
+  s2 = wave_sum_f64(s2);
+  a1 = wave_sum_f64(a1);
+  a2 = wave_sum_f64(a2);
+  const uint32_t nsum = (uint32_t)wave_sum_i((int32_t)na);
   if (lane == 0) {
-    red[0][wv] = sa;
-    red[1][wv] = st;
-    redn[wv] = na;
+    red[0][wv] = s1;
+    red[1][wv] = s2;
+    red[2][wv] = a1;
+    red[3][wv] = a2;
+    redn[wv] = nsum;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double a_ = 0.0, t_ = 0.0;
+    double S1 = 0.0, S2 = 0.0, A1 = 0.0, A2 = 0.0;
     uint64_t n_ = 0;
     for (int w = 0; w < kObWaves; ++w) {
-      a_ += red[0][w];
-      t_ += red[1][w];
+      S1 += red[0][w];
+      S2 += red[1][w];
+      A1 += red[2][w];
+      A2 += red[3][w];
       n_ += redn[w];
     }
     float mb, ma;
+    double d_;
     if (KIND == 0) {
-      mb = (float)(t_ - a_) / fmaxf((float)(P - (int64_t)n_), 1.0f);
-      ma = (float)a_ / fmaxf((float)n_, 1.0f);
+      const double B1 = S1 - A1, B2 = S2 - A2;
+      const double nb = (double)(P - (int64_t)n_), nab = (double)n_;
+      mb = (float)B1 / fmaxf((float)(P - (int64_t)n_), 1.0f);
+      ma = (float)A1 / fmaxf((float)n_, 1.0f);
+      const double mad = ma, mbd = mb;
+      d_ = (A2 - 2.0 * mad * A1 + nab * mad * mad) + (B2 - 2.0 * mbd * B1 + nb * mbd * mbd);
     } else {
-      const float norm1 = (float)a_;
+      const float norm1 = (float)S1;
       float scale;
       if (min_distortion) {
         scale = norm1 / (float)P;  // drive.py:61-62
       } else {
-        const float norm2 = (float)sqrt(t_);
+        const float norm2 = (float)sqrt(S2);
         const float n2sq = norm2 * norm2;
         scale = norm1 == 0.0f ? 0.0f : n2sq / norm1;  // drive.py:63-65 (divide_no_nan)
       }
       mb = -scale;
       ma = scale;
+      const double sd = scale;
+      // sum over x >= 0 of (x - s)^2 plus over x < 0 of (x + s)^2 = sum (|x| - s)^2
+      d_ = S2 - 2.0 * sd * S1 + (double)P * sd * sd;
     }
     means[2 * c] = mb;
     means[2 * c + 1] = ma;
-    mean_s[0] = mb;
-    mean_s[1] = ma;
-  }
-  __syncthreads();
-  const float mb = mean_s[0], ma = mean_s[1];
-  double dd = 0.0;
-  for (int64_t tt = wv; tt < ntile; tt += kObWaves) {
-    const int64_t tile = tt + t0 < ntile ? tt + t0 : tt + t0 - ntile;
-    const int64_t base = tile * 2048;
-    const bool full = base + 2048 <= P;
-    const float* __restrict__ xt = x + base + lane;
-    float fd = 0.0f;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float raw[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * g + j;
-        raw[j] = (full || base + 64 * k + lane < P) ? xt[64 * k] : 0.0f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * g + j;
-        const float v = raw[j] + 0.0f;
-        const float e = v - ((v < thr) ? mb : ma);
-        // elements past P: v = 0 decodes to a mean, so the term is dropped
-        fd += (full || base + 64 * k + lane < P) ? e * e : 0.0f;
-      }
-    }
-    dd += (double)fd;
-  }
-  dd = wave_sum_f64(dd);
-  if (lane == 0) red[2][wv] = dd;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double d_ = 0.0;
-    for (int w = 0; w < kObWaves; ++w) d_ += red[2][w];
-    dist[c] = d_;
+    dist[c] = d_ > 0.0 ? d_ : 0.0;
   }
 }
 
@@ -2628,6 +2644,12 @@ __global__ __launch_bounds__(256) void k_fwht_pass(float* const* rows, int64_t n
       x[e] = v;
     }
   }
+}
+
+// Measurement utility (bench.py): a plain 16-byte-per-lane grid-stride copy, the
+// achievable HBM streaming rate the codec kernels are compared with.
+__global__ __launch_bounds__(256) void k_copy_f4(uint4* __restrict__ dst, const uint4* __restrict__ src, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -2981,6 +3003,19 @@ int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, in
   return 0;
 }
 
+int fc_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
+  if (nbytes < 0 || (nbytes & 15) || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15))
+    return fail(-1, "fc_copy: 16-byte aligned pointers and a multiple of 16 bytes required");
+  if (nbytes == 0) return 0;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t n = nbytes / 16;
+  const dim3 grid((unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ncu * 8));
+  hipLaunchKernelGGL(k_copy_f4, grid, dim3(256), 0, (hipStream_t)stream, (uint4*)dst, (const uint4*)src, n);
+  return check_launch("k_copy_f4");
+}
+
 int fc_dequantize(const int32_t* sum, int64_t P, float step, const float* noise_sum, float* out,
                   void* stream) {
   if (P < 0) return fail(-1, "P < 0");
@@ -3002,11 +3037,16 @@ int fc_noise_sum(const int64_t* seeds, int32_t nclients, int64_t P, float* noise
 }
 
 int fc_client_norms(const float* const* xs, int32_t nclients, int64_t P, int kind, float* norms, void* stream) {
+  return fc_client_norms_scaled(xs, nclients, P, kind, nullptr, norms, stream);
+}
+
+int fc_client_norms_scaled(const float* const* xs, int32_t nclients, int64_t P, int kind, const float* prescale,
+                           float* norms, void* stream) {
   if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
-  if (kind < 1 || kind > 5) return fail(-1, "bad norm kind");
+  if (kind < 1 || kind > 6) return fail(-1, "bad norm kind");
   if (!xs || !norms) return fail(-1, "null pointer");
   hipLaunchKernelGGL(k_client_norms, dim3(nclients), dim3(kNormThreads), 0, (hipStream_t)stream, xs, P, kind,
-                     norms);
+                     prescale, norms);
   return check_launch("k_client_norms");
 }
 

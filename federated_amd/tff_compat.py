@@ -7,7 +7,8 @@ and ``next`` returns a ``MeasuredProcessOutput(state, result, measurements)``
 (``tff.templates.AggregationProcess`` / ``MeasuredProcessOutput`` as used at
 compressed_communication/aggregators/quantize_encode.py:161-213).  When TFF is
 present, ``federated_amd.tff_adapter`` (lazy import) wraps these into real TFF
-computations.
+computations (``quantize_encode_process`` / ``as_tff_factory``; untested here
+because TFF is absent).
 """
 import collections
 from typing import Any, Callable, Sequence

@@ -30,9 +30,10 @@
  *                          option quantize + dequantize distortion + code length
  *                          (quantize_encode_client_lambda.py:105-130), lengths only
  *   fc_noise_sum           federated_sum(noise) for dithered mode (quantize_encode.py:183)
- *   fc_client_norms        normalize_fn: mean_magnitude / max_magnitude /
+ *   fc_client_norms(_scaled) normalize_fn: mean_magnitude / max_magnitude /
  *                          dimensionless_norm (quantize_utils.py:20-29,
- *                          quantize_encode.py:79-90, 145)
+ *                          quantize_encode.py:79-90, 145); the clipping / zeroing
+ *                          wrapper norms of builder.py:100-117 (one fused pass)
  *   fc_finalize            avg_distortion / avg_sparsity / bit lengths per client
  *                          (quantize_encode.py:150-155, elias_gamma_encode.py:22-24, 100-108)
  *   fc_drive_encode        DRIVEFactory encode (comparison_methods/drive.py:58-76); its
@@ -67,6 +68,7 @@ extern "C" {
 /* Norms of the TFF wrappers restated by the builder (builder.py:104-117). */
 #define FC_NORM_L2 4   /* tf.linalg.global_norm: clipping_factory */
 #define FC_NORM_LINF 5 /* max |x|: zeroing_factory (norm_order=inf) */
+#define FC_NORM_L2_LINF 6 /* both wrapper norms in one pass: norms[c] = L2, norms[nclients + c] = LINF */
 
 #define FC_TILE_ELEMS 1024       /* encoder tile (one wavefront) = decoder index granularity */
 #define FC_MAX_ELEMS 67108863LL  /* P limit: 2^26 - 1 elements per client tensor */
@@ -172,6 +174,14 @@ int fc_noise_sum(const int64_t* seeds, int32_t nclients, int64_t P, float* noise
 int fc_client_norms(const float* const* xs, int32_t nclients, int64_t P, int kind,
                     float* norms, void* stream);
 
+/* fc_client_norms of the pre-scaled values (x * prescale[2c]) * prescale[2c+1]
+ * (prescale nullable, the same per-client pre-scales fc_quantize_encode takes):
+ * QuantizeEncode's normalize_fn sees the value after the TFF clipping and mean
+ * wrappers (builder.py:100-109 around quantize_encode.py:145).  kind
+ * FC_NORM_L2_LINF writes 2 * nclients floats. */
+int fc_client_norms_scaled(const float* const* xs, int32_t nclients, int64_t P, int kind,
+                           const float* prescale, float* norms, void* stream);
+
 /* Per-client reduction of the encoder's per-tile partials:
  * dist[c] = sum_t dist_part (float64), nnz[c] = sum_t nnz_part (int64). */
 int fc_finalize(const float* dist_part, const int32_t* nnz_part, int32_t nclients, int64_t P,
@@ -196,6 +206,11 @@ int fc_drive_encode(const float* const* xs, int32_t nclients, int64_t P, int min
  * the Rademacher signs of the Philox stream of (seed0, seed1). */
 int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, int64_t seed0,
                 int64_t seed1, void* stream);
+
+/* Measurement utility (not a reference interface): dst <- src, nbytes a multiple
+ * of 16, 16-byte aligned pointers; a grid-stride 16-byte-per-lane copy whose rate
+ * bench.py reports as the achievable HBM streaming peak beside the codec kernels. */
+int fc_copy(void* dst, const void* src, int64_t nbytes, void* stream);
 
 #ifdef __cplusplus
 }

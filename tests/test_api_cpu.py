@@ -101,6 +101,28 @@ def test_quantile_estimate_geometric_update():
   assert z.report(np.float32(10.0)) == 21.0
 
 
+def test_quantile_estimate_counts_against_the_raw_estimate():
+  # TFF applies multiplier / increment to the reported value only: the quantile
+  # query compares every record with the raw estimate X (10), not 2X + 1 (21).
+  z = builder.QuantileEstimate(10.0, 0.98, np.log(10.0), multiplier=2.0, increment=1.0)
+  norms = np.array([5.0, 9.0, 15.0, 20.0], np.float32)  # 2 of 4 <= X; all 4 <= 2X + 1
+  got = z.update(np.float32(10.0), norms)
+  want = np.float32(10.0) * np.exp(-np.float32(np.log(10.0)) * (np.float32(0.5) - np.float32(0.98)))
+  assert np.isclose(got, want, rtol=1e-6)
+  assert got > 10.0  # only half the clients are below X: the estimate grows
+
+
+def test_tff_adapter_imports_without_tff():
+  from federated_amd import tff_adapter  # pylint: disable=g-import-not-at-top
+  try:
+    import tensorflow_federated  # noqa: F401  pylint: disable=g-import-not-at-top,unused-import
+    pytest.skip("TFF present")
+  except ImportError:
+    pass
+  with pytest.raises(ImportError, match="tensorflow_federated"):
+    tff_adapter.as_tff_factory(quantize_encode.QuantizeEncodeFactory(0.5))
+
+
 # quantize_utils_test.py:157-186 (host scalar schedules of the product package)
 def test_product_schedules():
   assert [float(quantize_utils.linear_decay(2., 0., r, 4)) for r in range(4)] == [2., 1.5, 1., 0.5]

@@ -1,0 +1,195 @@
+"""GPU parity at every BASELINE.json configuration shape that fits one GPU.
+
+BASELINE.json ``configs`` (SURVEY.md §8 config sizes):
+  1. trainer.py plumbing: 16 clients x 1,206,590 (EMNIST CNN), trainer defaults
+     (uniform, step 0.5, clipping + zeroing on, weighted; trainer.py:63-90,
+     builder.py:453-525) through ``build_quantization_encode_aggregator``;
+  2. 128 clients x 2^20, stochastic "8-bit" (step 1/127, sigma 0.25);
+  3. 256 clients x 4,050,748 (StackOverflow LSTM), stochastic step 1.0;
+  headline: 1024 clients x 25,000,000, stochastic step 0.5 (bench.py's round),
+     and 257 clients x 25 M (more clients than decoder lanes per tile, an odd
+     client count for the encoder's multiply-high ticket division);
+  5. one-bit SGD codec at P = 25,000,000 (one_bit_sgd.py:45-112).
+Configs 4 and 5's 8-GPU splits are covered by the distributed tests.
+
+Checks, by what the oracle (CPU restatement) can afford in seconds:
+  * codes: byte-identical to the oracle for a subset of clients (all clients
+    where the oracle is fast enough);
+  * the round's int32 client sum: against the oracle's sum of every client where
+    affordable (configs 1-3), else against the sum of the HIP elementwise
+    quantiser ``fc_quantize`` (itself bit-exact against the oracle in
+    test_gpu_codec.py) -- a size-independent property of the full-size round;
+  * the dequantised sum: f32(sum) * step, bit-exact.
+"""
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+import torch
+
+from federated_amd import _lib
+from federated_amd import builder
+from federated_amd import codec
+from oracle import aggregators as oagg
+from oracle import codec as ocodec
+from oracle import quantize_utils as oq
+
+pytestmark = pytest.mark.gpu
+F32 = np.float32
+MODE = {"uniform": _lib.UNIFORM, "stochastic": _lib.STOCHASTIC}
+ORACLE_Q = {"uniform": lambda x, s, sd: oq.uniform_quantize(x, s), "stochastic": oq.stochastic_quantize}
+WORKERS = max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _host_deltas(C, P, sigma, seed):
+  def one(c):
+    return (np.random.default_rng(seed + c).standard_normal(P, dtype=np.float32) * F32(sigma))
+  with ThreadPoolExecutor(WORKERS) as ex:
+    return list(ex.map(one, range(C)))
+
+
+def _oracle_sum(xs, step, seeds, mode):
+  """int32 sum over clients of the oracle's q (thread pool: numpy releases the GIL)."""
+  def one(c):
+    return ORACLE_Q[mode](xs[c], F32(step), tuple(seeds[c])).astype(np.int64)
+  acc = np.zeros(xs[0].size, np.int64)
+  with ThreadPoolExecutor(WORKERS) as ex:
+    for q in ex.map(one, range(len(xs))):
+      acc += q
+  return oagg.wrap_i32(acc)
+
+
+def _hip_quantize_sum(rows, step, seeds, mode):
+  """int32 sum of fc_quantize (the oracle-pinned elementwise HIP quantiser)."""
+  acc = torch.zeros(rows[0].numel(), dtype=torch.int64, device=rows[0].device)
+  for c, r in enumerate(rows):
+    q, _ = codec.quantize(r, step, tuple(int(v) for v in seeds[c]), MODE[mode])
+    acc += q
+  return acc.to(torch.int32)
+
+
+def _check_codes(batch, xs_host, clients, step, seeds, mode):
+  for c in clients:
+    q = ORACLE_Q[mode](xs_host[c], F32(step), tuple(seeds[c]))
+    code, nbits = ocodec.run_length_gamma_encode(q)
+    assert int(batch.bits()[c]) == nbits, c
+    assert batch.client_code(c) == code, c
+
+
+def _round(rows, step, seeds, mode):
+  batch = codec.quantize_encode(rows, step, torch.from_numpy(seeds), MODE[mode])
+  ovf = codec.check_overflow(batch)
+  assert not len(ovf), ovf
+  out = torch.empty(rows[0].numel(), dtype=torch.float32, device=rows[0].device)
+  s, out, err = codec.decode_accumulate(batch, out=out, step=step)
+  assert int(err.item()) == 0
+  return batch, s, out
+
+
+def _release():
+  torch.cuda.synchronize()
+  torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("C,P,mode,step,sigma,code_clients", [
+    (128, 1 << 20, "stochastic", 1.0 / 127, 0.25, (0, 1, 64, 127)),          # config 2
+    (256, 4_050_748, "stochastic", 1.0, 1.0, (0, 1, 255)),                  # config 3
+], ids=["config2_128x1M_8bit", "config3_256x4.05M"])
+def test_config_round_matches_oracle(gpu, C, P, mode, step, sigma, code_clients):
+  xs = _host_deltas(C, P, sigma, seed=1000 * C)
+  seeds = np.array([[77 + c, 3 * c + 1] for c in range(C)], np.int64)
+  rows = [torch.from_numpy(x).to(gpu) for x in xs]
+  batch, s, out = _round(rows, step, seeds, mode)
+  _check_codes(batch, xs, code_clients, step, seeds, mode)
+  want = _oracle_sum(xs, step, seeds, mode)
+  np.testing.assert_array_equal(s.cpu().numpy(), want)
+  np.testing.assert_array_equal(out.cpu().numpy(), oq.uniform_dequantize(want, F32(step)))
+  del rows, batch
+  _release()
+
+
+@pytest.mark.parametrize("C,mode", [(257, "stochastic"), (1024, "stochastic"), (1024, "uniform")],
+                         ids=["257x25M_stochastic", "1024x25M_stochastic", "1024x25M_uniform"])
+def test_headline_shape_round(gpu, C, mode):
+  """25 M elements per client (24,415 tiles, look-backs across the whole client),
+  257 or 1024 clients: more clients than the decoder's 128 lanes per tile (each
+  lane walks several clients) and the encoder's ticket division at C = 257 / 1024."""
+  P, step = 25_000_000, 0.5
+  g = torch.Generator(device=gpu)
+  rows = []
+  for c in range(C):
+    g.manual_seed(4242 + c)
+    rows.append(torch.randn(P, generator=g, device=gpu, dtype=torch.float32))
+  seeds = np.array([[1000 + c, 1000 + c] for c in range(C)], np.int64)
+  batch, s, out = _round(rows, step, seeds, mode)
+  picks = (0, C // 2, C - 1)
+  _check_codes(batch, {c: rows[c].cpu().numpy() for c in picks}, picks, step, seeds, mode)
+  want = _hip_quantize_sum(rows, step, seeds, mode)
+  assert torch.equal(s, want)
+  np.testing.assert_array_equal(out.cpu().numpy(), oq.uniform_dequantize(want.cpu().numpy(), F32(step)))
+  # whole-batch code length: the sum of every client's bit count is what the decoder consumed
+  assert int(batch.bits().min()) > 0
+  del rows, batch, s, out, want
+  _release()
+
+
+def test_config1_trainer_defaults_round(gpu):
+  """trainer.py defaults (uniform, step 0.5, clipping + zeroing, weighted by example
+  counts) at the EMNIST CNN size, through the builder; oracle: the wrappers restated
+  in numpy around oracle.aggregators.quantize_encode_next."""
+  C, P = 16, 1_206_590
+  xs = _host_deltas(C, P, 0.02, seed=31)
+  xs[3] = xs[3] * F32(1000.0)  # a client far above the zeroing threshold
+  w = np.random.default_rng(5).integers(200, 2000, C).astype(np.float32)
+  f = builder.build_quantization_encode_aggregator()  # trainer defaults
+  process = f.create((np.float32, (P,)), (np.float32, ()))
+  state = process.initialize()
+  out = process.next(state, xs, weight=w)
+  # --- oracle: zeroing (linf > 2X + 1), clipping (global L2 vs C), mean weight ---
+  linf = np.array([np.max(np.abs(oq.ftz(x))) for x in xs], np.float32)
+  zero_thr = F32(F32(state["zeroing_norm"]) * F32(2.0) + F32(1.0))
+  keep = ~(linf > zero_thr)
+  assert not keep[3] and keep.sum() == C - 1
+  l2 = np.array([np.sqrt(np.sum(oq.ftz(x).astype(np.float64) ** 2)) for x in xs], np.float32)
+  l2 = np.where(keep, l2, F32(0.0)).astype(np.float32)
+  clip = F32(state["clipping_norm"])
+  with np.errstate(divide="ignore"):
+    inv = np.where(l2 > 0, F32(1.0) / l2, np.float32(np.inf)).astype(np.float32)
+  scale = np.where(keep, clip * np.minimum(inv, F32(1.0) / clip), F32(0.0)).astype(np.float32)
+  pre = [((x * scale[c]) * w[c]).astype(np.float32) for c, x in enumerate(xs)]
+  # uniform rounding draws no randomness: any seeds
+  want, meas, _ = oagg.quantize_encode_next(pre, 0.5, "uniform")
+  want = (want / F32(np.sum(w, dtype=np.float32))).astype(np.float32)
+  np.testing.assert_array_equal(out.result, want)
+  assert out.measurements["mean_value"]["avg_bitrate"] == meas["avg_bitrate"]
+  assert out.measurements["mean_value"]["avg_sparsity"] == meas["avg_sparsity"]
+  assert out.measurements["zeroing_norm"] == zero_thr
+  # next state: the quantile estimates moved against the raw estimates
+  assert out.state["clipping_norm"] == builder.QuantileEstimate(1.0, 0.8, 0.2).update(clip, l2)
+  _release()
+
+
+def test_config5_onebit_at_25M(gpu):
+  """One-bit SGD (config 5's codec) at P = 25 M: masks bit-exact, means and the
+  client-order float32 decoded sum against the oracle."""
+  C, P = 16, 25_000_000
+  xs = _host_deltas(C, P, 1.0, seed=555)
+  rows = [torch.from_numpy(x).to(gpu) for x in xs]
+  masks, means, dist = codec.onebit_encode(rows, 0.0)
+  nw = (P + 31) // 32
+  m = masks.cpu().numpy().view(np.uint32).reshape(C, nw)
+  for c in (0, C - 1):
+    # TF's mask word w holds element 32 w + i in bit i
+    bits = np.pad((xs[c] >= 0).astype(np.uint8), (0, nw * 32 - P)).reshape(nw, 32)
+    want = np.packbits(bits, axis=1, bitorder="little").view("<u4").reshape(-1)
+    np.testing.assert_array_equal(m[c], want)
+  res = codec.onebit_decode_sum(masks, means, C, P).cpu().numpy()
+  want, meas = oagg.one_bit_sgd_next(xs, 0.0)
+  np.testing.assert_allclose(means.cpu().numpy()[1::2],
+                             [F32(np.sum(x * (x >= 0), dtype=np.float64) / max(np.sum(x >= 0), 1))
+                              for x in xs], rtol=1e-6)
+  np.testing.assert_allclose(res, want, rtol=1e-5, atol=1e-5)
+  np.testing.assert_allclose(np.mean(dist.cpu().numpy()) / P, meas["avg_distortion"], rtol=1e-5)
+  del rows
+  _release()
