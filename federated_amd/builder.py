@@ -47,6 +47,9 @@ F32 = np.float32
 
 
 def _accepts(fn, name):
+  """Whether a process's next function takes keyword `name` (AggregationProcess.next
+  forwards *args / **kwargs: the wrapped next_fn's signature decides)."""
+  fn = getattr(getattr(fn, "__self__", None), "_next_fn", fn)
   try:
     return name in inspect.signature(fn).parameters
   except (TypeError, ValueError):

@@ -791,8 +791,11 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
       noise = u01(rbits[k]) - 0.5f;
       r = rintf(sc - noise);
     }
-    const float deq = (MODE == FC_DITHERED) ? (r + noise) * cq.step : r * cq.step;
-    const float dd = xv - deq;
+    // pow2 step (RCP): sc = x / step exactly, so x - deq = step * (sc - r') exactly
+    // (r' = r, or RN(r + noise) dithered) and every squared term and partial sum is
+    // the unscaled one times step^2 -- k_encode multiplies the tile sum by step^2
+    const float rq = (MODE == FC_DITHERED) ? (r + noise) : r;
+    const float dd = RCP ? sc - rq : xv - rq * cq.step;
     // zero padding past P quantises to 0; only dithering's noise would count
     dist = (!MASK || k < nvalid) ? fmaf(dd, dd, dist) : dist;
     q[k] = r;
@@ -1383,7 +1386,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
       const uint64_t fm = __ballot(lfirst >= 0);  // lanes are in element order
       const int32_t tile_first = fm ? __builtin_amdgcn_readlane(lfirst, (int)__builtin_ctzll(fm)) : -1;
       if (fast && !(FC_ABL & 32)) {
-        const float d = dsum;
+        const float d = RCP ? dsum * (cp.step * cp.step) : dsum;  // RCP: sums of (sc - r)^2
         const int32_t n = INT_IN ? wave_sum_i(nnz) : nnz;
         if (lane == 0) {
           if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
@@ -2131,7 +2134,9 @@ __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* cons
   const bool is_abs = kind == FC_NORM_MEAN_MAGNITUDE;
   const float s0 = prescale ? prescale[2 * c] : 1.0f, s1 = prescale ? prescale[2 * c + 1] : 1.0f;
   const int64_t ntile = (P + 2047) / 2048;
-  double acc = 0.0;
+  // eight independent float64 accumulators per lane (one per load slot): the
+  // float64 add latency stays off the critical path; summed in a fixed order
+  double accs[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   float mx = 0.0f;
   for (int64_t tile = wv; tile < ntile; tile += kNormThreads / 64) {
     const int64_t base = tile * 2048;
@@ -2152,10 +2157,11 @@ __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* cons
         const float a = fabsf(v);
         mx = fmaxf(mx, a);
         const double ad = (double)a;
-        acc += is_abs ? ad : ad * ad;
+        accs[j] = is_abs ? accs[j] + ad : fma(ad, ad, accs[j]);
       }
     }
   }
+  const double acc = ((accs[0] + accs[1]) + (accs[2] + accs[3])) + ((accs[4] + accs[5]) + (accs[6] + accs[7]));
   double r = is_max ? (double)mx : acc;
   float m = mx;
 #pragma unroll
@@ -2253,7 +2259,9 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
   const bool aligned = ((uintptr_t)x & 15u) == 0;
   // KIND 0: s1 = sum x, s2 = sum x^2, a1 / a2 = the same over x >= thr;
   // KIND 1: s1 = sum |x|, s2 = sum x^2
-  double s1 = 0.0, s2 = 0.0, a1 = 0.0, a2 = 0.0;
+  // one accumulator set per float4 component: independent float64 chains
+  double s1v[4] = {0.0, 0.0, 0.0, 0.0}, s2v[4] = {0.0, 0.0, 0.0, 0.0};
+  double a1v[4] = {0.0, 0.0, 0.0, 0.0}, a2v[4] = {0.0, 0.0, 0.0, 0.0};
   uint32_t na = 0;
   // clients start at different tiles: rows share their alignment, and reading
   // every client's same offset at once would load the same HBM channels
@@ -2288,14 +2296,14 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
         nib |= ab ? (1u << i) : 0u;
         const double vd = in ? (double)v : 0.0;
         if (KIND == 0) {
-          s1 += vd;
-          s2 = fma(vd, vd, s2);
+          s1v[i] += vd;
+          s2v[i] = fma(vd, vd, s2v[i]);
           const double t = ab ? vd : 0.0;
-          a1 += t;
-          a2 = fma(t, t, a2);
+          a1v[i] += t;
+          a2v[i] = fma(t, t, a2v[i]);
         } else {
-          s1 += fabs(vd);
-          s2 = fma(vd, vd, s2);
+          s1v[i] += fabs(vd);
+          s2v[i] = fma(vd, vd, s2v[i]);
         }
       }
       na += (uint32_t)__popc(nib);
@@ -2309,7 +2317,9 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
     const uint32_t word = wordbuf[wv][lane];
     if (tile * 64 + lane < nw) m[tile * 64 + lane] = word;
   }
-  // fixed-order reductions: lanes (DPP/shuffle tree), then waves in order
+  // fixed-order reductions: components, lanes (shuffle tree), then waves in order
+  double s1 = (s1v[0] + s1v[1]) + (s1v[2] + s1v[3]), s2 = (s2v[0] + s2v[1]) + (s2v[2] + s2v[3]);
+  double a1 = (a1v[0] + a1v[1]) + (a1v[2] + a1v[3]), a2 = (a2v[0] + a2v[1]) + (a2v[2] + a2v[3]);
   s1 = wave_sum_f64(s1);
   s2 = wave_sum_f64(s2);
   a1 = wave_sum_f64(a1);
@@ -2649,7 +2659,17 @@ __global__ __launch_bounds__(256) void k_fwht_pass(float* const* rows, int64_t n
 // Measurement utility (bench.py): a plain 16-byte-per-lane grid-stride copy, the
 // achievable HBM streaming rate the codec kernels are compared with.
 __global__ __launch_bounds__(256) void k_copy_f4(uint4* __restrict__ dst, const uint4* __restrict__ src, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+  // 4 x 16 B per lane in flight: all four loads issue before the stores
+  const int64_t stride = (int64_t)gridDim.x * 1024;
+  int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  for (; i + 768 < n; i += stride) {
+    const uint4 a = src[i], b = src[i + 256], c = src[i + 512], d = src[i + 768];
+    dst[i] = a;
+    dst[i + 256] = b;
+    dst[i + 512] = c;
+    dst[i + 768] = d;
+  }
+  for (; i < n; i += 256) dst[i] = src[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -2737,7 +2757,10 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   // few clients: cap the tiles in flight per client so look-back windows stay short
   // power-of-two step (no per-client normalisation): x / step == x * (1 / step)
   int ex = 0;
-  const bool pow2 = !int_in && !norms && std::frexp(step, &ex) == 0.5f && std::isnormal(1.0f / step);
+  // (step^2 normal too: the encoder's distortion partials are then step^2 times exact
+  // sums of (x / step - r)^2)
+  const bool pow2 = !int_in && !norms && std::frexp(step, &ex) == 0.5f && std::isnormal(1.0f / step) &&
+                    std::isnormal(step * step) && std::isfinite(step * step);
   a.rcp = pow2 ? 1.0f / step : 0.0f;
   void (*kern)(EncodeArgs) = nullptr;
   void (*exact)(EncodeArgs) = nullptr;
@@ -3011,7 +3034,7 @@ int fc_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t n = nbytes / 16;
-  const dim3 grid((unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ncu * 8));
+  const dim3 grid((unsigned)std::min<int64_t>((n + 1023) / 1024, (int64_t)ncu * 8));
   hipLaunchKernelGGL(k_copy_f4, grid, dim3(256), 0, (hipStream_t)stream, (uint4*)dst, (const uint4*)src, n);
   return check_launch("k_copy_f4");
 }
