@@ -10,7 +10,10 @@ OUT = os.path.join(HERE, "libfedcodec.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          # TF-CPU numerics: FTZ/DAZ on float32, no FMA contraction
-         "-fgpu-flush-denormals-to-zero", "-ffp-contract=off"]
+         "-fgpu-flush-denormals-to-zero", "-ffp-contract=off",
+         # no SLP packing into v_pk_* f32 ops: on gfx950 a v_pk_mul/add costs about two
+         # scalar ops plus the register moves it needs (k_encode -2.6 % without it)
+         "-fno-slp-vectorize"]
 
 
 def build(force=False, verbose=False):

@@ -2121,53 +2121,59 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // FC_NORM_L2_LINF: one pass for both wrapper norms, norms[c] = ||x||_2 and
 // norms[C + c] = max |x| (builder.py:100-117: clipping and zeroing).
 constexpr int kNormThreads = 1024;
-__global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* const* xs, int64_t P,
-                                                               int kind, const float* prescale,
-                                                               float* norms) {
+// ACC: 0 sum |x|, 1 sum x^2, 2 none (max only).  max |x| is always taken.
+template <int ACC, bool PRE>
+__global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* const* xs, int64_t P, int kind,
+                                                               const float* prescale, float* norms) {
   __shared__ double red[kNormThreads / 64];
   __shared__ float redm[kNormThreads / 64];
   const int c = blockIdx.x;
   const float* __restrict__ x = xs[c];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const bool both = kind == FC_NORM_L2_LINF;
-  const bool is_max = kind == FC_NORM_MAX_MAGNITUDE || kind == FC_NORM_LINF;
-  const bool is_abs = kind == FC_NORM_MEAN_MAGNITUDE;
-  const float s0 = prescale ? prescale[2 * c] : 1.0f, s1 = prescale ? prescale[2 * c + 1] : 1.0f;
+  const float s0 = PRE ? prescale[2 * c] : 1.0f, s1 = PRE ? prescale[2 * c + 1] : 1.0f;
+  const bool aligned = ((uintptr_t)x & 15u) == 0;
   const int64_t ntile = (P + 2047) / 2048;
-  // eight independent float64 accumulators per lane (one per load slot): the
-  // float64 add latency stays off the critical path; summed in a fixed order
-  double accs[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  // one float64 accumulator per float4 component: independent chains, summed in a
+  // fixed order
+  double acc4[4] = {0.0, 0.0, 0.0, 0.0};
   float mx = 0.0f;
   for (int64_t tile = wv; tile < ntile; tile += kNormThreads / 64) {
     const int64_t base = tile * 2048;
-    const bool full = base + 2048 <= P;
-    const float* __restrict__ xt = x + base + lane;
+    const bool full = base + 2048 <= P && aligned;
+    float4 raw[8];
+    if (full) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float raw[8];
+      for (int k = 0; k < 8; ++k) raw[k] = *(const float4*)(x + base + 256 * k + 4 * lane);
+    } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * g + j;
-        raw[j] = (full || base + 64 * k + lane < P) ? xt[64 * k] : 0.0f;
+      for (int k = 0; k < 8; ++k) {
+        const int64_t e = base + 256 * k + 4 * lane;
+        raw[k].x = e < P ? x[e] : 0.0f;
+        raw[k].y = e + 1 < P ? x[e + 1] : 0.0f;
+        raw[k].z = e + 2 < P ? x[e + 2] : 0.0f;
+        raw[k].w = e + 3 < P ? x[e + 3] : 0.0f;
       }
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float v = raw[j] + 0.0f;
-        if (prescale) v = (v * s0) * s1;
+    for (int k = 0; k < 8; ++k) {
+      const float v4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = v4[i] + 0.0f;  // DAZ as TF-CPU (zero padding past P adds nothing)
+        if (PRE) v = (v * s0) * s1;
         const float a = fabsf(v);
         mx = fmaxf(mx, a);
         const double ad = (double)a;
-        accs[j] = is_abs ? accs[j] + ad : fma(ad, ad, accs[j]);
+        if (ACC == 0) acc4[i] += ad;
+        if (ACC == 1) acc4[i] = fma(ad, ad, acc4[i]);
       }
     }
   }
-  const double acc = ((accs[0] + accs[1]) + (accs[2] + accs[3])) + ((accs[4] + accs[5]) + (accs[6] + accs[7]));
-  double r = is_max ? (double)mx : acc;
+  double r = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
   float m = mx;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const double v = shfl_xor_f64(r, o);
-    r = is_max ? fmax(r, v) : r + v;
+    r += shfl_xor_f64(r, o);
     m = fmaxf(m, __shfl_xor(m, o));
   }
   if (lane == 0) {
@@ -2179,14 +2185,15 @@ __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* cons
     double t = red[0];
     float tm = redm[0];
     for (int w = 1; w < kNormThreads / 64; ++w) {
-      t = is_max ? fmax(t, red[w]) : t + red[w];
+      t += red[w];
       tm = fmaxf(tm, redm[w]);
     }
-    if (kind == FC_NORM_MEAN_MAGNITUDE) t = t / (double)P;
-    if (kind == FC_NORM_DIMENSIONLESS) t = sqrt(t / (double)P);
-    if (kind == FC_NORM_L2 || both) t = sqrt(t);
-    norms[c] = (float)t;
-    if (both) norms[gridDim.x + c] = tm;
+    float out = tm;  // FC_NORM_MAX_MAGNITUDE / FC_NORM_LINF
+    if (kind == FC_NORM_MEAN_MAGNITUDE) out = (float)(t / (double)P);
+    if (kind == FC_NORM_DIMENSIONLESS) out = (float)sqrt(t / (double)P);
+    if (kind == FC_NORM_L2 || kind == FC_NORM_L2_LINF) out = (float)sqrt(t);
+    norms[c] = out;
+    if (kind == FC_NORM_L2_LINF) norms[gridDim.x + c] = tm;
   }
 }
 
@@ -2290,11 +2297,12 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
       uint32_t nib = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bool in = full || e + i < P;
+        // zero padding past P (v = 0) adds nothing to the sums; only the mask bit
+        // and the count need the bound
         const float v = v4[i];
-        const bool ab = in && !(v < thr);
+        const bool ab = (full || e + i < P) && !(v < thr);
         nib |= ab ? (1u << i) : 0u;
-        const double vd = in ? (double)v : 0.0;
+        const double vd = (double)v;
         if (KIND == 0) {
           s1v[i] += vd;
           s2v[i] = fma(vd, vd, s2v[i]);
@@ -3068,8 +3076,11 @@ int fc_client_norms_scaled(const float* const* xs, int32_t nclients, int64_t P, 
   if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
   if (kind < 1 || kind > 6) return fail(-1, "bad norm kind");
   if (!xs || !norms) return fail(-1, "null pointer");
-  hipLaunchKernelGGL(k_client_norms, dim3(nclients), dim3(kNormThreads), 0, (hipStream_t)stream, xs, P, kind,
-                     prescale, norms);
+  const int acc = kind == FC_NORM_MEAN_MAGNITUDE ? 0 : (kind == FC_NORM_MAX_MAGNITUDE || kind == FC_NORM_LINF) ? 2 : 1;
+  void (*kern)(const float* const*, int64_t, int, const float*, float*) =
+      prescale ? (acc == 0 ? k_client_norms<0, true> : acc == 1 ? k_client_norms<1, true> : k_client_norms<2, true>)
+               : (acc == 0 ? k_client_norms<0, false> : acc == 1 ? k_client_norms<1, false> : k_client_norms<2, false>);
+  hipLaunchKernelGGL(kern, dim3(nclients), dim3(kNormThreads), 0, (hipStream_t)stream, xs, P, kind, prescale, norms);
   return check_launch("k_client_norms");
 }
 

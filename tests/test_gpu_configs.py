@@ -78,7 +78,9 @@ def _check_codes(batch, xs_host, clients, step, seeds, mode):
 
 
 def _round(rows, step, seeds, mode):
-  batch = codec.quantize_encode(rows, step, torch.from_numpy(seeds), MODE[mode])
+  # default capacities (4 bits/element): wider codes (config 2's ~10 bits) overflow and
+  # exercise the re-encode of just the overflowed clients
+  batch = codec.quantize_encode_checked(rows, step, torch.from_numpy(seeds), MODE[mode])
   ovf = codec.check_overflow(batch)
   assert not len(ovf), ovf
   out = torch.empty(rows[0].numel(), dtype=torch.float32, device=rows[0].device)
