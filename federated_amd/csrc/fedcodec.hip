@@ -349,6 +349,15 @@ __device__ __forceinline__ uint32_t dpp_incl_sum(uint32_t x) {
   x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return x;
 }
+__device__ __forceinline__ uint32_t dpp_incl_or(uint32_t x) {
+  x |= __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x |= __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x |= __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x |= __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x |= __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x |= __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
 __device__ __forceinline__ int32_t dpp_incl_max(int32_t x) {
   const int32_t id = (int32_t)0x80000000;
   x = max(x, __builtin_amdgcn_update_dpp(id, x, 0x111, 0xf, 0xf, false));
@@ -655,16 +664,29 @@ __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t,
   const int32_t M = dpp_incl_max(lastv);
   const int32_t Mx = dpp_shr1(M, -1);  // last nonzero before this tile
   uint32_t contrib = agg ? l1 : 0u;
-  if (nz) contrib += glen((uint32_t)(tb + (int32_t)fr - Mx));
-  const uint32_t csum = (uint32_t)wave_sum_i((int32_t)contrib);
+  const uint32_t dfirst = (uint32_t)(tb + (int32_t)fr - Mx);  // nz lanes: their first run value
+  if (nz) contrib += glen(dfirst);
+  const uint32_t incl = dpp_incl_sum(contrib);
+  const uint32_t csum = (uint32_t)lane63((int32_t)incl);
   r.last = lane63(M);
   r.body = pbody + csum;
   if (__builtin_amdgcn_readlane(l1, 63) >= 32u) {  // the newest body holds the last 32 bits
     r.tail = __builtin_amdgcn_readlane(l2, 63);
     return r;
   }
+  // short newest body (nearly empty tiles, e.g. sparse clients): the last 32 bits
+  // gather from several pieces.  Piece i (lanes >= p) is lane i's run code + body
+  // (the prefix lane: its stream tail); S = csum - incl bits follow it; a piece with
+  // S < 32 contributes (its low bits << S), and the pieces' bits are disjoint, so
+  // the tail is the OR over lanes.  (A piece's tail holds its last <= 32 body bits,
+  // zero above a shorter body.)
   FC_COUNT(11, 1);
-  return lookback(status_c, t, lane, slow);  // short newest body: exact scalar fold
+  const uint32_t S = csum - incl;
+  uint64_t v = (uint64_t)l2;
+  if (nz && l1 < 32u) v |= (uint64_t)dfirst << l1;
+  const uint32_t cpart = (lane >= p && S < 32u) ? (uint32_t)(v << S) : 0u;
+  r.tail = (uint32_t)lane63((int32_t)dpp_incl_or(cpart));
+  return r;
 }
 
 // Runtime-indexed read of a small register array without scratch (select chain).
@@ -762,7 +784,24 @@ __device__ __forceinline__ float vmax3_abs(float a, float b, float c) {
 // its exponent, and the in-chunk run lengths come from select chains on the
 // nonzero flags.  |r| >= 8192, Inf or NaN marks the chunk long; the slow path
 // then recomputes the tile exactly (TF cast semantics, codes of any length).
-template <int MODE, bool RCP, bool PRE, bool MASK = false>
+// DIV: how x / step is formed (all three equal to TF-CPU's IEEE division on the
+// fast path's range): 0 the IEEE division; 1 step a power of two, x * (1 / step)
+// is exact; 2 step known to the host with a significand other than all ones:
+// q0 = x * y, r = x - q0 * step (exact, one FMA), q = RN(q0 + r * y) with
+// y = RN(1 / step) -- Markstein's theorem makes q the correctly rounded quotient
+// (normal range; quotients beyond the fast path's |q| < 8192 or under 2^-125 do
+// not change q and the exact path recomputes anything it marks long).
+template <int DIV>
+__device__ __forceinline__ float div_step(float x, float step, float y) {
+  if (DIV == 1) return x * y;
+  if (DIV == 2) {
+    const float q0 = x * y;
+    return fmaf(fmaf(-q0, step, x), y, q0);
+  }
+  return x / step;
+}
+
+template <int MODE, int DIV, bool PRE, bool MASK = false>
 __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t g,
                                                      const uint32_t (&r4)[4], int32_t rel0,
                                                      float& dist, int32_t& nnz, const uint32_t* clut,
@@ -780,7 +819,7 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
   for (int k = 0; k < 4; ++k) {
     float xv = __uint_as_float(r4[k]);
     if (PRE) xv = (xv * cq.s0) * cq.s1;
-    const float sc = RCP ? xv * cq.rcp : xv / cq.step;
+    const float sc = div_step<DIV>(xv, cq.step, cq.rcp);
     float r, noise = 0.0f;
     if (MODE == FC_UNIFORM) {
       r = rintf(sc);
@@ -795,7 +834,7 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
     // (r' = r, or RN(r + noise) dithered) and every squared term and partial sum is
     // the unscaled one times step^2 -- k_encode multiplies the tile sum by step^2
     const float rq = (MODE == FC_DITHERED) ? (r + noise) : r;
-    const float dd = RCP ? sc - rq : xv - rq * cq.step;
+    const float dd = DIV == 1 ? sc - rq : xv - rq * cq.step;
     // zero padding past P quantises to 0; only dithering's noise would count
     dist = (!MASK || k < nvalid) ? fmaf(dd, dd, dist) : dist;
     q[k] = r;
@@ -1200,7 +1239,7 @@ __device__ __forceinline__ uint4 stage_read(const uint32_t* stg, int lane, int j
 // predecessor status was fetched before tile n's work) finishes its look-back
 // and stores its words -- so the look-back's memory round trip overlaps a
 // whole tile of compute instead of stalling the wave.
-template <int MODE, bool INT_IN, bool RCP, bool PRE>
+template <int MODE, bool INT_IN, int DIV, bool PRE>
 __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs a) {
   __shared__ uint32_t wins[2][kWinWords + 3];  // double-buffered; + guard words
   __shared__ uint32_t clut[kCodeLut];
@@ -1331,10 +1370,10 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
           } else {
             const uint32_t g = (uint32_t)((tile_base + rel0) >> 2);
             if (MODE == FC_DITHERED && !full)
-              cc = quant_code_fast<MODE, RCP, PRE, true>(cq, g, raw[j], rel0, dist, nnz, clut,
+              cc = quant_code_fast<MODE, DIV, PRE, true>(cq, g, raw[j], rel0, dist, nnz, clut,
                                                     (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - rel0)));
             else
-              cc = quant_code_fast<MODE, RCP, PRE>(cq, g, raw[j], rel0, dist, nnz, clut);
+              cc = quant_code_fast<MODE, DIV, PRE>(cq, g, raw[j], rel0, dist, nnz, clut);
           }
           chunk_prepend(cc, llast);  // no-op without an earlier nonzero in the lane
           lfirst = lfirst < 0 ? cc.first : lfirst;
@@ -1386,7 +1425,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
       const uint64_t fm = __ballot(lfirst >= 0);  // lanes are in element order
       const int32_t tile_first = fm ? __builtin_amdgcn_readlane(lfirst, (int)__builtin_ctzll(fm)) : -1;
       if (fast && !(FC_ABL & 32)) {
-        const float d = RCP ? dsum * (cp.step * cp.step) : dsum;  // RCP: sums of (sc - r)^2
+        const float d = DIV == 1 ? dsum * (cp.step * cp.step) : dsum;  // DIV 1: sums of (sc - r)^2
         const int32_t n = INT_IN ? wave_sum_i(nnz) : nnz;
         if (lane == 0) {
           if (a.dist_part) a.dist_part[(int64_t)c * a.T + t] = d;
@@ -2769,16 +2808,25 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   // sums of (x / step - r)^2)
   const bool pow2 = !int_in && !norms && std::frexp(step, &ex) == 0.5f && std::isnormal(1.0f / step) &&
                     std::isnormal(step * step) && std::isfinite(step * step);
-  a.rcp = pow2 ? 1.0f / step : 0.0f;
+  // a host-known step that is not a power of two: Markstein's correctly rounded
+  // quotient from RN(1 / step) (not for an all-ones significand, where the
+  // remainder x - q0 * step is not exact)
+  uint32_t sbits = 0;
+  std::memcpy(&sbits, &step, 4);
+  const bool mark = !int_in && !norms && !pow2 && std::isnormal(step) && std::isnormal(1.0f / step) &&
+                    (sbits & 0x7FFFFFu) != 0x7FFFFFu;
+  a.rcp = (pow2 || mark) ? 1.0f / step : 0.0f;
   void (*kern)(EncodeArgs) = nullptr;
   void (*exact)(EncodeArgs) = nullptr;
   const bool pre = !int_in && prescale != nullptr;
-#define FC_PICK(M, I, R, Q) (kern = k_encode<M, I, R, Q>, exact = k_encode_exact<M, I, R>)
-#define FC_PICK2(M, R) (pre ? FC_PICK(M, false, R, true) : FC_PICK(M, false, R, false))
-  if (int_in) FC_PICK(FC_UNIFORM, true, false, false);
-  else if (mode == FC_UNIFORM) pow2 ? FC_PICK2(FC_UNIFORM, true) : FC_PICK2(FC_UNIFORM, false);
-  else if (mode == FC_STOCHASTIC) pow2 ? FC_PICK2(FC_STOCHASTIC, true) : FC_PICK2(FC_STOCHASTIC, false);
-  else pow2 ? FC_PICK2(FC_DITHERED, true) : FC_PICK2(FC_DITHERED, false);
+#define FC_PICK(M, I, D, Q) (kern = k_encode<M, I, D, Q>, exact = k_encode_exact<M, I, D == 1>)
+#define FC_PICK2(M, D) (pre ? FC_PICK(M, false, D, true) : FC_PICK(M, false, D, false))
+#define FC_PICK3(M) (pow2 ? FC_PICK2(M, 1) : mark ? FC_PICK2(M, 2) : FC_PICK2(M, 0))
+  if (int_in) FC_PICK(FC_UNIFORM, true, 0, false);
+  else if (mode == FC_UNIFORM) FC_PICK3(FC_UNIFORM);
+  else if (mode == FC_STOCHASTIC) FC_PICK3(FC_STOCHASTIC);
+  else FC_PICK3(FC_DITHERED);
+#undef FC_PICK3
 #undef FC_PICK2
 #undef FC_PICK
   {  // ticket -> (tile, client) by multiply-high

@@ -215,3 +215,32 @@ def test_noise_sum_many_clients(gpu):
     want = want + oq.generate_noise(tuple(seeds[c]), P)
   got = codec.noise_sum(torch.from_numpy(seeds), P, gpu).cpu().numpy()
   np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("step", [1.0 / 127, 0.4, 0.1, 1.0 / 3, 0.7, 3.7e-3, 0.275, 1.9999999])
+@pytest.mark.parametrize("mode", ["uniform", "stochastic"])
+def test_encoder_division_matches_ieee_over_whole_binades(gpu, step, mode):
+  """The encoder forms x / step without a division for host-known steps (a
+  multiply for powers of two; Markstein's RN(1/step) + FMA remainder correction
+  otherwise; the IEEE division for an all-ones significand such as 1.9999999).
+  Every float32 of whole binades of x (|x / step| in [1, 2), [63, 128) and
+  [4096, 8192), both signs: 2^25 consecutive bit patterns plus the tie points)
+  must quantise exactly as the elementwise kernel, which divides with the IEEE
+  division and is bit-exact against the oracle (test_quantize_matches_oracle)."""
+  s = np.float32(step)
+  parts = []
+  for k, sign in ((0, 1), (6, -1), (12, 1)):
+    lo = np.float32(s * np.float32(2.0**k)).view(np.uint32)
+    bits = lo + np.arange(1 << 23, dtype=np.uint32)
+    parts.append(bits.view(np.float32) * np.float32(sign))
+  ties = (np.arange(-3000, 3000, dtype=np.float32) + np.float32(0.5)) * s
+  x = np.concatenate(parts + [ties, np.nextafter(ties, np.float32(np.inf)),
+                              np.nextafter(ties, np.float32(-np.inf))]).astype(np.float32)
+  xt = torch.from_numpy(x).to(gpu)
+  seed = (12, 34)
+  batch = codec.quantize_encode_checked([xt], float(s), torch.tensor([seed], dtype=torch.int64), MODES[mode])
+  got, _, err = codec.decode_accumulate(batch)
+  assert int(err.item()) == 0
+  want, _ = codec.quantize(xt, float(s), seed, MODES[mode])
+  bad = torch.nonzero(got != want).flatten()
+  assert bad.numel() == 0, (x[bad[:5].cpu().numpy()], got[bad[:5]].cpu(), want[bad[:5]].cpu())
