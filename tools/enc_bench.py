@@ -16,36 +16,41 @@ P = int(os.environ.get("P", 25_000_000))
 C = int(os.environ.get("C", 1024))
 MODE = int(os.environ.get("MODE", _lib.STOCHASTIC))
 STEP = float(os.environ.get("STEP", 0.5))
-SIGMA = float(os.environ.get("SIGMA", 1.0))
+SIGMAS = [float(v) for v in os.environ.get("SIGMA", "1.0").split(",")]
 REPS = int(os.environ.get("REPS", 5))
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev)
 rows = []
 for c in range(C):
   g.manual_seed(77 + c)
-  rows.append(torch.randn(P, generator=g, device=dev).mul_(SIGMA))
+  rows.append(torch.randn(P, generator=g, device=dev))
 ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
 seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
 batch = codec.EncodedBatch(P, C, [int(P * float(os.environ.get("CAP", 1.0))) + 1024] * C, dev)
 out = torch.empty(P, dtype=torch.float32, device=dev)
 err = torch.zeros(1, dtype=torch.int32, device=dev)
-s = torch.cuda.current_stream()
-enc, dec = [], []
-for it in range(REPS + 1):
-  e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-  e[0].record(s)
-  codec.quantize_encode(None, STEP, seeds, MODE, ptrs=ptrs, P=P, out=batch, stream=s)
-  e[1].record(s)
-  codec.decode_accumulate(batch, want_sum=False, out=out, step=STEP, err=err, stream=s)
-  e[2].record(s)
-  torch.cuda.synchronize()
-  if it:
-    enc.append(e[0].elapsed_time(e[1]))
-    dec.append(e[1].elapsed_time(e[2]))
-enc.sort()
-dec.sort()
-bits = float(batch.bits().sum()) / (C * P)
-ok = not len(codec.check_overflow(batch)) and int(err.item()) == 0
-print("%-28s C=%d P=%d mode=%d step=%g  encode %.3f ms  decode %.3f ms  %.3f bits/elt  %s" % (
-    os.path.basename(_lib.LIB_PATH), C, P, MODE, STEP, enc[len(enc) // 2], dec[len(dec) // 2], bits,
-    "ok" if ok else "ERROR"), flush=True)
+prev = 1.0
+for SIGMA in SIGMAS:
+  for r in rows:
+    r.mul_(SIGMA / prev)
+  prev = SIGMA if SIGMA else 1.0
+  s = torch.cuda.current_stream()
+  enc, dec = [], []
+  for it in range(REPS + 1):
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    e[0].record(s)
+    codec.quantize_encode(None, STEP, seeds, MODE, ptrs=ptrs, P=P, out=batch, stream=s)
+    e[1].record(s)
+    codec.decode_accumulate(batch, want_sum=False, out=out, step=STEP, err=err, stream=s)
+    e[2].record(s)
+    torch.cuda.synchronize()
+    if it:
+      enc.append(e[0].elapsed_time(e[1]))
+      dec.append(e[1].elapsed_time(e[2]))
+  enc.sort()
+  dec.sort()
+  bits = float(batch.bits().sum()) / (C * P)
+  ok = not len(codec.check_overflow(batch)) and int(err.item()) == 0
+  print("%-28s C=%d P=%d mode=%d step=%g sigma=%g  encode %.3f ms  decode %.3f ms  %.3f bits/elt  %s" % (
+      os.path.basename(_lib.LIB_PATH), C, P, MODE, STEP, SIGMA, enc[len(enc) // 2], dec[len(dec) // 2], bits,
+      "ok" if ok else "ERROR"), flush=True)

@@ -23,7 +23,8 @@ dev = torch.device("cuda:0")
 g = torch.Generator(device=dev)
 g.manual_seed(1)
 NPOOL = int(os.environ.get("POOL", 4)) or C  # POOL=0: a distinct delta per client
-pool = [torch.randn(P, generator=g, device=dev) for _ in range(NPOOL)]
+SIGMA = float(os.environ.get("SIGMA", 1.0))
+pool = [torch.randn(P, generator=g, device=dev).mul_(SIGMA) for _ in range(NPOOL)]
 rows = [pool[c % NPOOL] for c in range(C)]
 ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
 seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
@@ -34,7 +35,7 @@ for it in range(3):
     lib.fc_debug_stamps(buf, 1)
   torch.cuda.synchronize()
   t0 = time.perf_counter()
-  codec.quantize_encode(None, 0.5, seeds, mode, ptrs=ptrs, P=P, out=batch)
+  codec.quantize_encode(None, float(os.environ.get("STEP", 0.5)), seeds, mode, ptrs=ptrs, P=P, out=batch)
   torch.cuda.synchronize()
   dt = time.perf_counter() - t0
   if HAVE:
