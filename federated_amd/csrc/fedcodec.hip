@@ -1802,6 +1802,9 @@ constexpr int kDecChunk = FC_DEC_CHUNK;  // 16-byte blocks per chunk (one 64-B l
 #ifndef FC_DEC_LONG
 #define FC_DEC_LONG 4
 #endif
+#ifndef FC_DEC_LONG_LANES
+#define FC_DEC_LONG_LANES 16  // waiting lanes that trigger an arithmetic slot before its turn
+#endif
 #ifndef FC_DEC_STEPS
 #define FC_DEC_STEPS 2
 #endif
@@ -1975,7 +1978,10 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     // pair running past the segment end) decodes one code arithmetically -- only on
     // every kDecLong-th iteration, so the wave runs that block rarely instead of
     // whenever any of its 64 lanes needs it; the lane idles meanwhile.
-    if (moved == 0 && (it & (kDecLong - 1)) == 0) {
+    // (or at once when a quarter of the wave is waiting: streams of long codes,
+    // e.g. 8-bit steps, would otherwise decode one code every kDecLong iterations)
+    const bool idle = moved == 0;
+    if (idle && ((it & (kDecLong - 1)) == 0 || __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES)) {
       // right after a refill (>= 33 window bits): one code decoded arithmetically --
       // near the segment end, or a code longer than 12 bits
       const uint32_t top = (uint32_t)(r.win >> 32);
