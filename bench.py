@@ -53,6 +53,7 @@ sys.path.insert(0, ROOT)
 
 from federated_amd import _lib  # noqa: E402
 from federated_amd import codec  # noqa: E402
+from federated_amd import distributed  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 MODES = {"uniform": _lib.UNIFORM, "stochastic": _lib.STOCHASTIC, "dithered": _lib.DITHERED}
@@ -407,9 +408,7 @@ def main():
   if world > 1:
     import torch.distributed as dist  # pylint: disable=g-import-not-at-top
 
-  T = codec.num_tiles(P)
-  nslab = max(1, min(args.slabs, T))
-  bounds = [T * k // nslab for k in range(nslab + 1)]
+  bounds = distributed.slab_bounds(codec.num_tiles(P), args.slabs)  # shrinking: the last is smallest
 
   def step():
     codec.quantize_encode(None, args.step_size, seeds, mode, ptrs=ptrs, P=P, out=batch,
@@ -422,10 +421,10 @@ def main():
       # the decode) while range k+1 decodes; the int32 sum is exact in any order
       err.zero_()
       works = []
-      for k in range(nslab):
+      for k in range(len(bounds) - 1):
         codec.decode_accumulate(batch, sum_out=isum, err=err, stream=stream,
                                 tiles=(bounds[k], bounds[k + 1]))
-        lo, hi = bounds[k] * 1024, min(P, bounds[k + 1] * 1024)
+        lo, hi = distributed.slab_elements(bounds, k, P)
         works.append(dist.all_reduce(isum[lo:hi], async_op=True))
       for w in works:
         w.wait()

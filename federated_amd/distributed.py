@@ -30,12 +30,44 @@ def allreduce_sum_(t, group=None):
   return t
 
 
+def slab_bounds(T, n):
+  """Tile boundaries of `n` decode slabs over T tiles, shrinking towards the end.
+
+  Slab k gets a share proportional to n - k (e.g. 4:3:2:1 of the tiles for n = 4):
+  every slab's all-reduce overlaps the decode of the next one, so only the last
+  slab's all-reduce (and the dequantise) is exposed, and the last slab is the
+  smallest.  Returns n + 1 increasing boundaries from 0 to T (empty slabs are
+  dropped when T < n).
+  """
+  T, n = int(T), max(1, int(n))
+  w = [n - k for k in range(n)]
+  tot = sum(w)
+  b = [0]
+  acc = 0
+  for k in range(n):
+    acc += w[k]
+    b.append((T * acc) // tot)
+  out = [b[0]]
+  for x in b[1:]:
+    if x > out[-1]:
+      out.append(x)
+  if out[-1] != T:
+    out.append(T)
+  return out
+
+
+def slab_elements(bounds, k, P, tile=1024):
+  """Element range [lo, hi) of slab k (the last tile may be partial)."""
+  return bounds[k] * tile, min(int(P), bounds[k + 1] * tile)
+
+
 def aggregate_round(local_rows, step, local_seeds, mode, group=None, prescale=None, slabs=4):
   """Encode + decode this rank's clients, all-reduce the int32 sums, dequantise.
 
-  The decode runs in `slabs` tile ranges (fc_decode_accumulate_tiles); each
-  range's sum is all-reduced asynchronously (the collective's stream waits for
-  that range's decode) while the next range decodes.  Integer sums make the
+  The decode runs in `slabs` tile ranges (fc_decode_accumulate_tiles, shrinking
+  ones: slab_bounds); each range's sum is all-reduced asynchronously (the
+  collective's stream waits for that range's decode) while the next range
+  decodes.  Integer sums make the
   result independent of the range split and of the ring order.
   Returns (float32 result [P], local EncodedBatch).  Dithered mode also
   all-reduces the float32 noise sum (tolerance, as TFF's federated_sum).
@@ -45,14 +77,12 @@ def aggregate_round(local_rows, step, local_seeds, mode, group=None, prescale=No
   isum = torch.empty(P, dtype=torch.int32, device=batch.device)
   err = torch.zeros(1, dtype=torch.int32, device=batch.device)
   multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
-  T = codec.num_tiles(P)
-  n = max(1, min(int(slabs), T)) if multi else 1
-  bounds = [T * k // n for k in range(n + 1)]
+  bounds = slab_bounds(codec.num_tiles(P), slabs if multi else 1)
   works = []
-  for k in range(n):
+  for k in range(len(bounds) - 1):
     codec.decode_accumulate(batch, sum_out=isum, err=err, tiles=(bounds[k], bounds[k + 1]))
     if multi:
-      lo, hi = bounds[k] * 1024, min(P, bounds[k + 1] * 1024)
+      lo, hi = slab_elements(bounds, k, P)
       works.append(dist.all_reduce(isum[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True))
   for w in works:
     w.wait()
