@@ -2293,7 +2293,10 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const float* dist_part, c
 // Inputs pass through `+ 0.0f` so denormals flush as on TF-CPU before the
 // comparison.  KIND 0: one-bit SGD (threshold thr, class means).  KIND 1: DRIVE
 // (mask = !(x < 0), scale from sum |x| and sum x^2, means -scale / +scale).
-constexpr int kObThreads = 256;
+#ifndef FC_OB_THREADS
+#define FC_OB_THREADS 256
+#endif
+constexpr int kObThreads = FC_OB_THREADS;
 constexpr int kObWaves = kObThreads / 64;
 
 __device__ __forceinline__ uint32_t dpp_row_shl(uint32_t x, int n) {
@@ -2318,19 +2321,19 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
   const int64_t ntile = (P + 2047) / 2048;
   const bool aligned = ((uintptr_t)x & 15u) == 0;
   // KIND 0: s1 = sum x, s2 = sum x^2, a1 / a2 = the same over x >= thr;
-  // KIND 1: s1 = sum |x|, s2 = sum x^2
-  // one accumulator set per float4 component: independent float64 chains
-  double s1v[4] = {0.0, 0.0, 0.0, 0.0}, s2v[4] = {0.0, 0.0, 0.0, 0.0};
-  double a1v[4] = {0.0, 0.0, 0.0, 0.0}, a2v[4] = {0.0, 0.0, 0.0, 0.0};
+  // KIND 1: s1 = sum |x|, s2 = sum x^2.  Sums of x: float32 partials over a
+  // tile's 32 elements per lane, float64 across tiles; sums of squares in float64
+  // throughout (x^2 exact: the distortion below subtracts nearly equal terms).
+  // Fixed order everywhere.
+  double s1 = 0.0, s2 = 0.0, a1 = 0.0, a2 = 0.0;
   uint32_t na = 0;
   // clients start at different tiles: rows share their alignment, and reading
   // every client's same offset at once would load the same HBM channels
   const int64_t t0 = ((int64_t)c * 977) % ntile;
-  for (int64_t tt = wv; tt < ntile; tt += kObWaves) {
-    const int64_t tile = tt + t0 < ntile ? tt + t0 : tt + t0 - ntile;
+  auto tile_of = [&](int64_t tt) { return tt + t0 < ntile ? tt + t0 : tt + t0 - ntile; };
+  auto load_tile = [&](int64_t tile, float4 (&raw)[8]) {
     const int64_t base = tile * 2048;
     const bool full = base + 2048 <= P && aligned;
-    float4 raw[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int64_t e = base + 256 * k + 4 * lane;
@@ -2343,6 +2346,12 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
         raw[k].w = e + 3 < P ? x[e + 3] : 0.0f;
       }
     }
+  };
+  auto do_tile = [&](int64_t tile, const float4 (&raw)[8]) {
+    const int64_t base = tile * 2048;
+    const bool full = base + 2048 <= P;
+    float p1 = 0.0f, q1 = 0.0f;
+    double p2[2] = {0.0, 0.0}, q2[2] = {0.0, 0.0};  // two chains each
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int64_t e = base + 256 * k + 4 * lane;
@@ -2357,14 +2366,15 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
         nib |= ab ? (1u << i) : 0u;
         const double vd = (double)v;
         if (KIND == 0) {
-          s1v[i] += vd;
-          s2v[i] = fma(vd, vd, s2v[i]);
-          const double t = ab ? vd : 0.0;
-          a1v[i] += t;
-          a2v[i] = fma(t, t, a2v[i]);
+          p1 += v;
+          p2[k & 1] = fma(vd, vd, p2[k & 1]);
+          const float t = ab ? v : 0.0f;
+          q1 += t;
+          const double td = ab ? vd : 0.0;
+          q2[k & 1] = fma(td, td, q2[k & 1]);
         } else {
-          s1v[i] += fabs(vd);
-          s2v[i] = fma(vd, vd, s2v[i]);
+          p1 += fabsf(v);
+          p2[k & 1] = fma(vd, vd, p2[k & 1]);
         }
       }
       na += (uint32_t)__popc(nib);
@@ -2374,13 +2384,28 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
       wd |= dpp_row_shl(wd, 4) << 16;
       if ((lane & 7) == 0) wordbuf[wv][8 * k + (lane >> 3)] = wd;
     }
+    s1 += (double)p1;
+    s2 += p2[0] + p2[1];
+    if (KIND == 0) {
+      a1 += (double)q1;
+      a2 += q2[0] + q2[1];
+    }
     __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses execute in order
     const uint32_t word = wordbuf[wv][lane];
     if (tile * 64 + lane < nw) m[tile * 64 + lane] = word;
+  };
+  // software-pipelined: the next tile's loads are in flight while a tile computes
+  float4 ra[8], rb[8];
+  if (wv < ntile) load_tile(tile_of(wv), ra);
+  for (int64_t tt = wv; tt < ntile; tt += 2 * kObWaves) {
+    const int64_t tn = tt + kObWaves;
+    if (tn < ntile) load_tile(tile_of(tn), rb);
+    do_tile(tile_of(tt), ra);
+    if (tn >= ntile) break;
+    if (tn + kObWaves < ntile) load_tile(tile_of(tn + kObWaves), ra);
+    do_tile(tile_of(tn), rb);
   }
-  // fixed-order reductions: components, lanes (shuffle tree), then waves in order
-  double s1 = (s1v[0] + s1v[1]) + (s1v[2] + s1v[3]), s2 = (s2v[0] + s2v[1]) + (s2v[2] + s2v[3]);
-  double a1 = (a1v[0] + a1v[1]) + (a1v[2] + a1v[3]), a2 = (a2v[0] + a2v[1]) + (a2v[2] + a2v[3]);
+  // fixed-order reductions: lanes (shuffle tree), then waves in order
   s1 = wave_sum_f64(s1);
   s2 = wave_sum_f64(s2);
   a1 = wave_sum_f64(a1);

@@ -1,60 +1,74 @@
-"""Copy a tools/profile_bench.sh run into profiles/<round>/ (kernel stats, PMC summary, traffic.json).
+"""Copy tools/profile_workloads.sh runs into profiles/<round>/ (kernel stats, traffic per workload).
 
-python tools/make_profile_record.py gpurun_out/prof_xxx profiles/r01 --clients 1024 --P 25000000 \
-    --mode stochastic --step 0.5 --command "..."
+python tools/make_profile_record.py gpurun_out/prof profiles/r02 [workload ...]
 
-traffic.json holds per-dispatch HBM bytes for k_encode / k_decode with the gfx950
-correction of MI355X_MICROARCH.md's HBM section: FETCH_SIZE x2 for the encoder's
-wide streaming reads, FETCH_SIZE as-is for the decoder's narrow 16-B reads, plus
-WRITE_SIZE (both in KiB from rocprofv3).
+For each workload <w>: profiles/<round>/kernel_stats_<w>.csv (rocprofv3
+--kernel-trace --stats of `bench.py --workload <w>`) and traffic_<w>.json: per
+kernel, the mean per-dispatch FETCH_SIZE / WRITE_SIZE (KiB, separate --pmc
+passes) and the HBM bytes per launch with MI355X_MICROARCH.md's gfx950
+correction -- FETCH_SIZE x2 for wide (16-byte-per-lane) coalesced streaming
+reads (k_encode's LDS-DMA staging, k_client_norms' float4 loads), FETCH_SIZE
+as-is for the decoder's scattered 16-byte reads and for 4-byte-per-lane loads
+(k_mask_encode; each input byte is read once, so its algorithmic bytes
+calibrate the factor: see `calib`), plus WRITE_SIZE.  bench.py reads these
+files for the roofline's `traffic`.
 """
-import argparse
 import csv
 import glob
 import json
 import os
 import shutil
+import sys
 from collections import defaultdict
+
+KERNELS = {  # name fragment -> (key, FETCH multiplier)
+    "::k_encode<": ("k_encode", 2.0),
+    "k_decode<": ("k_decode", 1.0),
+    "k_client_norms": ("k_client_norms", 2.0),
+    "k_mask_encode<": ("k_mask_encode", 1.0),
+    "k_onebit_decode_sum": ("k_onebit_decode_sum", 1.0),
+}
+
+
+def kernel_key(name):
+  if "k_encode_exact" in name:
+    return None
+  for frag, (key, mult) in KERNELS.items():
+    if frag in name:
+      return key, mult
+  return None
 
 
 def main():
-  ap = argparse.ArgumentParser()
-  ap.add_argument("src")
-  ap.add_argument("dst")
-  ap.add_argument("--clients", type=int, default=1024)
-  ap.add_argument("--P", type=int, default=25_000_000)
-  ap.add_argument("--mode", default="stochastic")
-  ap.add_argument("--step", type=float, default=0.5)
-  ap.add_argument("--command", default="tools/profile_bench.sh <out> --steps 3 --warmup 1")
-  a = ap.parse_args()
-  os.makedirs(a.dst, exist_ok=True)
-  ks = glob.glob(os.path.join(a.src, "kt", "**", "*kernel_stats.csv"), recursive=True)
-  shutil.copy(ks[0], os.path.join(a.dst, "kernel_stats.csv"))
-  summ = os.path.join(a.src, "summary.txt")
-  if os.path.exists(summ):
-    shutil.copy(summ, os.path.join(a.dst, "pmc_summary.txt"))
-  per = defaultdict(lambda: defaultdict(list))
-  for f in glob.glob(os.path.join(a.src, "**", "*counter_collection.csv"), recursive=True):
-    with open(f) as fh:
-      for row in csv.DictReader(fh):
-        name = row["Kernel_Name"]
-        key = "k_encode" if "k_encode<" in name else (
-            "k_decode" if ("k_decode(" in name or "k_decode<" in name) else None)
-        if key:
-          per[key][row["Counter_Name"]].append(float(row["Counter_Value"]))
-  out = {}
-  for key, d in per.items():
-    fetch = sum(d["FETCH_SIZE"]) / max(1, len(d["FETCH_SIZE"]))
-    write = sum(d["WRITE_SIZE"]) / max(1, len(d["WRITE_SIZE"]))
-    mult = 2.0 if key == "k_encode" else 1.0
-    out[key] = {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write,
-                "hbm_bytes_corrected": (mult * fetch + write) * 1024.0,
-                "correction": ("FETCH x2 (gfx950 wide streaming read, MI355X_MICROARCH.md HBM section) + WRITE"
-                               if mult == 2.0 else "FETCH (narrow scattered 16-B reads: no x2) + WRITE")}
-  out["config"] = {"clients": a.clients, "P": a.P, "mode": a.mode, "step": a.step, "command": a.command}
-  with open(os.path.join(a.dst, "traffic.json"), "w") as fh:
-    json.dump(out, fh, indent=1)
-  print(json.dumps(out, indent=1))
+  src, dst = sys.argv[1], sys.argv[2]
+  wls = sys.argv[3:] or sorted(d for d in os.listdir(src) if os.path.isdir(os.path.join(src, d)))
+  os.makedirs(dst, exist_ok=True)
+  for w in wls:
+    base = os.path.join(src, w)
+    ks = glob.glob(os.path.join(base, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    if ks:
+      shutil.copy(ks[0], os.path.join(dst, "kernel_stats_%s.csv" % w))
+    per = defaultdict(lambda: defaultdict(list))
+    mults = {}
+    for f in glob.glob(os.path.join(base, "**", "*counter_collection.csv"), recursive=True):
+      with open(f) as fh:
+        for row in csv.DictReader(fh):
+          k = kernel_key(row["Kernel_Name"])
+          if k:
+            per[k[0]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            mults[k[0]] = k[1]
+    out = {}
+    for key, d in per.items():
+      fetch = sum(d["FETCH_SIZE"]) / max(1, len(d["FETCH_SIZE"]))
+      write = sum(d["WRITE_SIZE"]) / max(1, len(d["WRITE_SIZE"]))
+      m = mults[key]
+      out[key] = {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write, "dispatches": len(d["FETCH_SIZE"]),
+                  "fetch_multiplier": m, "hbm_bytes_corrected": (m * fetch + write) * 1024.0}
+    out["workload"] = w
+    out["command"] = "tools/profile_workloads.sh <out> %s (bench.py --workload %s)" % (w, w)
+    with open(os.path.join(dst, "traffic_%s.json" % w), "w") as fh:
+      json.dump(out, fh, indent=1)
+    print(w, json.dumps({k: round(v["hbm_bytes_corrected"] / 1e9, 3) for k, v in out.items() if isinstance(v, dict)}))
 
 
 if __name__ == "__main__":

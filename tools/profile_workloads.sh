@@ -1,0 +1,18 @@
+#!/bin/bash
+# rocprofv3 records of bench.py workloads: a kernel-trace summary and separate
+# FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md: one TCC counter group per
+# pass), per workload.  usage: bash tools/profile_workloads.sh <outdir> [workload ...]
+set -e
+OUT=$1; shift
+WL=${@:-headline headline_uniform trainer_round config2 config3 onebit}
+export TMPDIR=/tmp
+mkdir -p $OUT
+for w in $WL; do
+  A="--workload $w --no-cpu-baseline --steps 3 --warmup 1 --extra-steps 3"
+  mkdir -p $OUT/$w
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$w/kt -o run -- python3 bench.py $A > $OUT/$w/kt.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$w/fetch -o run -- python3 bench.py $A > $OUT/$w/fetch.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$w/write -o run -- python3 bench.py $A > $OUT/$w/write.log 2>&1
+  echo "profiled $w"
+done
+echo PROFILE_DONE
