@@ -20,7 +20,9 @@ quantiser sees exactly the step TF would compute from the same norm.
 Parity: q and the bitstream are bit-exact against the oracle given the norm;
 the norm itself is TF's float32 reduction in an unspecified order (here a
 correctly rounded float64 sum), and the server's float32 sum over clients is
-order-dependent, so both are compared within a tolerance.
+order-dependent (its order, and so its last bits, may also vary from run to
+run: the decoder adds the clients it decodes side by side with LDS float
+atomics), so both are compared within a tolerance.
 """
 import collections
 

@@ -143,8 +143,10 @@ int fc_decode_accumulate_tiles(const uint8_t* stream_buf, const int64_t* stream_
                                const float* noise_sum, int32_t* err, void* stream);
 
 /* QSGD server side: out[i] = [fsum_in[i] +] sum over clients of
- * float(q_c[i]) * client_scale[c] in float32 (summation order unspecified: the
- * reference's client-order float sum is matched within a tolerance). */
+ * float(q_c[i]) * client_scale[c] in float32.  The summation order is
+ * unspecified and may differ run to run (LDS float atomics over the clients
+ * decoded side by side), so the last bits of out may too; the reference's
+ * client-order float sum is matched within a tolerance. */
 int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream_off,
                                 const int64_t* stream_cap, const uint64_t* idx, int32_t nclients,
                                 int64_t P, const float* client_scale, const float* fsum_in,

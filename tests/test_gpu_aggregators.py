@@ -239,6 +239,10 @@ def test_qsgd_matches_oracle(gpu, P, C):
   assert out.measurements["avg_bitrate"] == m["avg_bitrate"]
   assert out.measurements["avg_sparsity"] == m["avg_sparsity"]
   np.testing.assert_allclose(out.measurements["avg_distortion"], m["avg_distortion"], rtol=1e-5)
+  # the float32 client sum uses LDS float atomics: its order -- and so
+  # its last bits -- may vary run to run; the variation stays within the same bound
+  out2 = process.next(process.initialize(), xs, seeds=seeds)
+  np.testing.assert_allclose(out2.result, out.result, rtol=2e-6 * C, atol=2e-6 * C * scale)
 
 
 def test_qsgd_codes_bit_exact(gpu):
