@@ -2190,21 +2190,26 @@ __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* cons
   // fixed order
   double acc4[4] = {0.0, 0.0, 0.0, 0.0};
   float mx = 0.0f;
+  // global (not flat) loads of the client's row
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) float* gfptr;
+  typedef const __attribute__((address_space(1))) f4v* gf4ptr;
+  const gfptr xg = (gfptr)x;
   for (int64_t tile = wv; tile < ntile; tile += kNormThreads / 64) {
     const int64_t base = tile * 2048;
     const bool full = base + 2048 <= P && aligned;
-    float4 raw[8];
+    f4v raw[8];
     if (full) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) raw[k] = *(const float4*)(x + base + 256 * k + 4 * lane);
+      for (int k = 0; k < 8; ++k) raw[k] = *(gf4ptr)(xg + base + 256 * k + 4 * lane);
     } else {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int64_t e = base + 256 * k + 4 * lane;
-        raw[k].x = e < P ? x[e] : 0.0f;
-        raw[k].y = e + 1 < P ? x[e + 1] : 0.0f;
-        raw[k].z = e + 2 < P ? x[e + 2] : 0.0f;
-        raw[k].w = e + 3 < P ? x[e + 3] : 0.0f;
+        raw[k].x = e < P ? xg[e] : 0.0f;
+        raw[k].y = e + 1 < P ? xg[e + 1] : 0.0f;
+        raw[k].z = e + 2 < P ? xg[e + 2] : 0.0f;
+        raw[k].w = e + 3 < P ? xg[e + 3] : 0.0f;
       }
     }
 #pragma unroll
@@ -2329,25 +2334,34 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
   uint32_t na = 0;
   // clients start at different tiles: rows share their alignment, and reading
   // every client's same offset at once would load the same HBM channels
-  const int64_t t0 = ((int64_t)c * 977) % ntile;
+#ifndef FC_OB_ROTATE
+#define FC_OB_ROTATE 1
+#endif
+  const int64_t t0 = FC_OB_ROTATE ? ((int64_t)c * 977) % ntile : 0;
   auto tile_of = [&](int64_t tt) { return tt + t0 < ntile ? tt + t0 : tt + t0 - ntile; };
-  auto load_tile = [&](int64_t tile, float4 (&raw)[8]) {
+  // global (not flat) loads: a flat load also counts in lgkmcnt, so every LDS
+  // wait of the word assembly would wait for the in-flight tile too
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) float* gfptr;
+  typedef const __attribute__((address_space(1))) f4v* gf4ptr;
+  const gfptr xg = (gfptr)x;
+  auto load_tile = [&](int64_t tile, f4v (&raw)[8]) {
     const int64_t base = tile * 2048;
-    const bool full = base + 2048 <= P && aligned;
+    if (base + 2048 <= P && aligned) {  // wave-uniform: 8 float4 loads, no branches
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int64_t e = base + 256 * k + 4 * lane;
-      if (full) {
-        raw[k] = *(const float4*)(x + e);
-      } else {
-        raw[k].x = e < P ? x[e] : 0.0f;
-        raw[k].y = e + 1 < P ? x[e + 1] : 0.0f;
-        raw[k].z = e + 2 < P ? x[e + 2] : 0.0f;
-        raw[k].w = e + 3 < P ? x[e + 3] : 0.0f;
+      for (int k = 0; k < 8; ++k) raw[k] = *(gf4ptr)(xg + base + 256 * k + 4 * lane);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int64_t e = base + 256 * k + 4 * lane;
+        raw[k].x = e < P ? xg[e] : 0.0f;
+        raw[k].y = e + 1 < P ? xg[e + 1] : 0.0f;
+        raw[k].z = e + 2 < P ? xg[e + 2] : 0.0f;
+        raw[k].w = e + 3 < P ? xg[e + 3] : 0.0f;
       }
     }
   };
-  auto do_tile = [&](int64_t tile, const float4 (&raw)[8]) {
+  auto do_tile = [&](int64_t tile, const f4v (&raw)[8]) {
     const int64_t base = tile * 2048;
     const bool full = base + 2048 <= P;
     float p1 = 0.0f, q1 = 0.0f;
@@ -2395,7 +2409,7 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
     if (tile * 64 + lane < nw) m[tile * 64 + lane] = word;
   };
   // software-pipelined: the next tile's loads are in flight while a tile computes
-  float4 ra[8], rb[8];
+  f4v ra[8], rb[8];
   if (wv < ntile) load_tile(tile_of(wv), ra);
   for (int64_t tt = wv; tt < ntile; tt += 2 * kObWaves) {
     const int64_t tn = tt + kObWaves;
