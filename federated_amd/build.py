@@ -13,7 +13,12 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-fgpu-flush-denormals-to-zero", "-ffp-contract=off",
          # no SLP packing into v_pk_* f32 ops: on gfx950 a v_pk_mul/add costs about two
          # scalar ops plus the register moves it needs (k_encode -2.6 % without it)
-         "-fno-slp-vectorize"]
+         "-fno-slp-vectorize",
+         # no atomic optimizer: its expansion (mbcnt, readfirstlane of the result right
+         # after the atomic) made k_encode wait for each ticket atomic -- and every
+         # vector memory operation before it -- where it is issued instead of where
+         # the ticket is used, a tile later
+         "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
 
 
 def build(force=False, verbose=False):

@@ -1286,8 +1286,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
     const bool have = ticket < total_tiles;
     if (!have && !pv) break;
     STAMP(0);
-    uint32_t ntk = 0;
-    if (ticket1 < total_tiles && lane == 0) ntk = atomicAdd(my_counter, 1u);  // ticket after next
+    uint32_t ntk = 0;  // the ticket after next: requested once the next tile is staged (below)
     // the pending tile's look-back window (lane i: tile pt-64+i), fetched now and
     // used after this tile's work
     uint64_t pw1 = 0, pw2 = 0;  // not fetched: unreadable (lookback_vec re-polls it if needed)
@@ -1352,6 +1351,10 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
       }
       // the staging is free once read: stage the next tile (waited for after part C)
       staged = ticket1 < total_tiles && stage_tile(a, cparams, ticket1, stg, lane);
+      // ticket after next: its round trip completes under this tile's work (the
+      // s_waitcnt after part C); requested at the loop top it made every tile wait
+      // for the atomic and for the previous tile's stores
+      if (ticket1 < total_tiles && lane == 0) ntk = atomicAdd(my_counter, 1u);
       // ---- A: quantise + code the lane's four chunks in order.  A chunk's first
       //      run code comes from the lane's previous nonzero when there is one;
       //      the lane's very first run code depends on earlier lanes and is
