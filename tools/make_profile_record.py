@@ -7,10 +7,10 @@ For each workload <w>: profiles/<round>/kernel_stats_<w>.csv (rocprofv3
 kernel, the mean per-dispatch FETCH_SIZE / WRITE_SIZE (KiB, separate --pmc
 passes) and the HBM bytes per launch with MI355X_MICROARCH.md's gfx950
 correction -- FETCH_SIZE x2 for wide (16-byte-per-lane) coalesced streaming
-reads (k_encode's LDS-DMA staging, k_client_norms' float4 loads), FETCH_SIZE
-as-is for the decoder's scattered 16-byte reads and for 4-byte-per-lane loads
-(k_mask_encode; each input byte is read once, so its algorithmic bytes
-calibrate the factor: see `calib`), plus WRITE_SIZE.  bench.py reads these
+reads (k_encode's LDS-DMA staging, the float4 row loads of k_client_norms and
+k_mask_encode -- each of their input bytes is read once, so the algorithmic
+bytes confirm the factor), FETCH_SIZE as-is for the decoder's scattered
+16-byte reads, plus WRITE_SIZE.  bench.py reads these
 files for the roofline's `traffic`.
 """
 import csv
@@ -25,7 +25,7 @@ KERNELS = {  # name fragment -> (key, FETCH multiplier)
     "::k_encode<": ("k_encode", 2.0),
     "k_decode<": ("k_decode", 1.0),
     "k_client_norms": ("k_client_norms", 2.0),
-    "k_mask_encode<": ("k_mask_encode", 1.0),
+    "k_mask_encode<": ("k_mask_encode", 2.0),
     "k_onebit_decode_sum": ("k_onebit_decode_sum", 1.0),
 }
 
@@ -39,7 +39,24 @@ def kernel_key(name):
   return None
 
 
+def recorrect(path):
+  """Recompute hbm_bytes_corrected of a recorded traffic_<w>.json with KERNELS' multipliers."""
+  with open(path) as fh:
+    d = json.load(fh)
+  mult = {key: m for key, m in KERNELS.values()}
+  for k, v in d.items():
+    if isinstance(v, dict) and k in mult:
+      v["fetch_multiplier"] = mult[k]
+      v["hbm_bytes_corrected"] = (mult[k] * v["FETCH_SIZE_KB"] + v["WRITE_SIZE_KB"]) * 1024.0
+  with open(path, "w") as fh:
+    json.dump(d, fh, indent=1)
+
+
 def main():
+  if sys.argv[1] == "--recorrect":
+    for f in sys.argv[2:]:
+      recorrect(f)
+    return
   src, dst = sys.argv[1], sys.argv[2]
   wls = sys.argv[3:] or sorted(d for d in os.listdir(src) if os.path.isdir(os.path.join(src, d)))
   os.makedirs(dst, exist_ok=True)
