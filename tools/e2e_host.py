@@ -7,7 +7,10 @@ both.  Clients are copied from pinned host buffers in batches on a copy stream
 while the previous batch encodes (double-buffered), then decoded and the f32
 result copied back.
 
-usage: python tools/e2e_host.py [--clients 64] [--batch 16] [--P 25000000]
+--codec onebit: config 5's codec (one-bit SGD, one_bit_sgd.py:45-112): the batches
+are mask-encoded as they arrive, the server sum decodes all clients in order.
+
+usage: python tools/e2e_host.py [--clients 64] [--batch 16] [--P 25000000] [--codec rlgamma|onebit]
 """
 import argparse
 import json
@@ -27,6 +30,7 @@ def main():
   ap.add_argument("--batch", type=int, default=16)
   ap.add_argument("--P", type=int, default=25_000_000)
   ap.add_argument("--reps", type=int, default=3)
+  ap.add_argument("--codec", default="rlgamma", choices=["rlgamma", "onebit"])
   args = ap.parse_args()
   dev = torch.device("cuda:0")
   C, B, P = args.clients, args.batch, args.P
@@ -38,11 +42,18 @@ def main():
   comp_s = torch.cuda.current_stream()
   seeds = torch.tensor([[c, c] for c in range(B)], dtype=torch.int64, device=dev)
   cap = codec._round_up(P + 256, 64)
-  batches = [codec.EncodedBatch(P, B, [cap] * B, dev) for _ in range(C // B)]
+  batches = [codec.EncodedBatch(P, B, [cap] * B, dev) for _ in range(C // B)] if args.codec == "rlgamma" else []
   out = torch.empty(P, device=dev)
   isum = torch.zeros(P, dtype=torch.int32, device=dev)
   err = torch.zeros(1, dtype=torch.int32, device=dev)
   out_host = torch.empty(P).pin_memory()
+  onebit = args.codec == "onebit"
+  nw = (P + 31) // 32
+  if onebit:
+    masks = torch.empty(C * nw, dtype=torch.int32, device=dev)
+    means = torch.empty(2 * C, dtype=torch.float32, device=dev)
+    dist = torch.empty(C, dtype=torch.float64, device=dev)
+  h = _lib.stream_handle(comp_s)
 
   def round_once():
     ev = [torch.cuda.Event() for _ in range(2)]
@@ -61,7 +72,16 @@ def main():
             dbuf[1 - cur][i].copy_(host[i], non_blocking=True)
           ev[1 - cur].record(copy_s)
       ptrs = torch.tensor([t.data_ptr() for t in dbuf[cur]], dtype=torch.int64, device=dev)
-      codec.quantize_encode(None, 0.5, seeds, _lib.STOCHASTIC, ptrs=ptrs, P=P, out=batches[k], stream=comp_s)
+      if onebit:
+        _lib.call("fc_onebit_encode", _lib.ptr(ptrs), B, P, 0.0, _lib.ptr(masks[k * B * nw:]),
+                  _lib.ptr(means[2 * k * B:]), _lib.ptr(dist[k * B:]), h)
+      else:
+        codec.quantize_encode(None, 0.5, seeds, _lib.STOCHASTIC, ptrs=ptrs, P=P, out=batches[k], stream=comp_s)
+    if onebit:
+      _lib.call("fc_onebit_decode_sum", _lib.ptr(masks), _lib.ptr(means), C, P, _lib.ptr(out), h)
+      out_host.copy_(out, non_blocking=True)
+      torch.cuda.synchronize()
+      return
     for k in range(nb):
       last = k == nb - 1
       codec.decode_accumulate(batches[k], sum_in=isum if k else None, sum_out=None if last else isum,
@@ -77,7 +97,8 @@ def main():
     round_once()
     ts.append(time.perf_counter() - t0)
   t = min(ts)
-  print(json.dumps({"metric": "host-resident round (H2D + encode + decode + D2H)", "clients": C, "P": P,
+  print(json.dumps({"metric": "host-resident round (H2D + encode + decode + D2H)", "codec": args.codec,
+                    "clients": C, "P": P,
                     "seconds": round(t, 4), "GiB_per_s": round(C * P * 4 / t / 2**30, 2),
                     "h2d_GB": round(C * P * 4 / 1e9, 2)}))
 
