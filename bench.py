@@ -26,6 +26,9 @@ launch / its launch time vs the 8 TB/s HBM peak):
                     into the encoder, decode, weighted mean (builder.py:77-117)
   config2           128 x 2^20, stochastic step 1/127, sigma 0.25 ("8-bit")
   config3           256 x 4,050,748 (StackOverflow LSTM), stochastic step 1.0
+  config4_share     one GPU's share of config 4 (512 x 11 M over 8 GPUs): 64 x 11 M,
+                    stochastic step 0.5 (sigma 1)
+  headline_c128     one GPU's share of the 8-GPU headline: 128 x 25 M
   onebit            config 5's codec: 1024 x 25 M one-bit SGD (one_bit_sgd.py:45-112)
   copy              a 16-byte-per-lane HBM copy (the achievable streaming rate)
 ``--workload NAME`` runs one of them alone (for rocprofv3 passes of one workload).
@@ -57,7 +60,8 @@ from federated_amd import distributed  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 MODES = {"uniform": _lib.UNIFORM, "stochastic": _lib.STOCHASTIC, "dithered": _lib.DITHERED}
-EXTRA = ["headline_uniform", "trainer_round", "config2", "config3", "onebit", "copy"]
+EXTRA = ["headline_uniform", "trainer_round", "config2", "config3", "config4_share", "headline_c128", "onebit",
+         "copy"]
 
 
 def parse():
@@ -354,9 +358,15 @@ def run_extra(name, args, dev, stream, head_rows, head_ptrs):
     return w_onebit(head_rows, head_ptrs, P, steps, warmup, stream)
   if name == "copy":
     return w_copy(dev, stream)
+  if name == "headline_c128":  # the first 128 of the headline's client deltas
+    return codec_round(name, head_rows[:128], head_ptrs[:128], P, 0.5, _lib.STOCHASTIC, max(steps, 10), warmup,
+                       stream)
   if name == "config2":
     rows = make_deltas(128, 1 << 20, 0.25, dev, 7000)
     step = 1.0 / 127
+  elif name == "config4_share":
+    rows = make_deltas(64, 11_000_000, 1.0, dev, 11000)
+    step = 0.5
   else:  # config3
     rows = make_deltas(256, 4_050_748, 1.0, dev, 9000)
     step = 1.0
@@ -384,7 +394,7 @@ def main():
   g.manual_seed(20251015 + rank)
   npool = args.pool if args.pool > 0 else Cg
   pool = []
-  need_head = not single or args.workload in ("headline_uniform", "trainer_round", "onebit")
+  need_head = not single or args.workload in ("headline_uniform", "trainer_round", "onebit", "headline_c128")
   for i in range(npool if need_head else 0):
     if npool == Cg:  # a delta per client, seeded by its global index: any --gpus N sums the same round
       g.manual_seed(20251015 + rank * Cg + i)

@@ -4,7 +4,7 @@
 # pass), per workload.  usage: bash tools/profile_workloads.sh <outdir> [workload ...]
 set -e
 OUT=$1; shift
-WL=${@:-headline headline_uniform trainer_round config2 config3 onebit}
+WL=${@:-headline headline_uniform trainer_round config2 config3 config4_share headline_c128 onebit}
 export TMPDIR=/tmp
 mkdir -p $OUT
 for w in $WL; do
