@@ -585,9 +585,12 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
 // first run code length, and the sum of bodies.  The combined tail is the
 // newest tile's tail whenever that tile's body has >= 32 bits; otherwise the
 // scalar lookback() does the fold.  No prefix within 64 tiles: lookback_deep().
-__device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t, int lane,
-                                            bool& slow, uint64_t pre1,
-                                            uint64_t pre2) {
+__device__ __noinline__ Seg lookback_vec_wait(const uint64_t* status_c, int32_t t, int lane, uint64_t pre1,
+                                              uint64_t pre2);
+template <bool WAIT>
+__device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32_t t, int lane,
+                                                 bool& slow, uint64_t pre1,
+                                                 uint64_t pre2) {
   // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
   // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
   const int32_t ti = t - 64 + lane;
@@ -598,9 +601,25 @@ __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t,
   }
   // a status is readable once both granules carry the same nonzero flag
   bool valid = h1 >= 0x40000000u && (h1 ^ h2) < 0x40000000u;
-  uint32_t spins = 0;
   int p;
-  for (;;) {
+  if (!WAIT) {
+    // common case: the prefetched window already holds a prefix and every
+    // aggregate after it (no loop, so no lane-mask phi in the caller's loop)
+    const uint64_t pre = __ballot(valid && h1 >= 0x80000000u);
+    const uint64_t val = __ballot(valid);
+    p = pre ? 63 - (int)__clzll(pre) : 0;
+    const uint64_t need = ~0ull << p;
+    if (pre == 0 || (val & need) != need) {
+      Seg r = lookback_vec_wait(status_c, t, lane, pre1, pre2);
+      if (r.has_nz == kSegSlow) {
+        slow = true;
+        r = seg_identity();
+      }
+      return r;
+    }
+  }
+  uint32_t spins = 0;
+  for (; WAIT;) {
     const uint64_t pre = __ballot(valid && h1 >= 0x80000000u);  // inclusive prefix (or slow)
     const uint64_t val = __ballot(valid);
     if (pre == 0) {  // no prefix in the window: walk 64-tile windows
@@ -687,6 +706,19 @@ __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t,
   const uint32_t cpart = (lane >= p && S < 32u) ? (uint32_t)(v << S) : 0u;
   r.tail = (uint32_t)lane63((int32_t)dpp_incl_or(cpart));
   return r;
+}
+
+// The waiting variant, out of line (a re-poll, or no prefix in the window).
+__device__ __noinline__ Seg lookback_vec_wait(const uint64_t* status_c, int32_t t, int lane, uint64_t pre1,
+                                              uint64_t pre2) {
+  bool slow = false;
+  Seg r = lookback_vec_impl<true>(status_c, t, lane, slow, pre1, pre2);
+  if (slow) r.has_nz = kSegSlow;
+  return r;
+}
+__device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t, int lane, bool& slow,
+                                            uint64_t pre1, uint64_t pre2) {
+  return lookback_vec_impl<false>(status_c, t, lane, slow, pre1, pre2);
 }
 
 // Runtime-indexed read of a small register array without scratch (select chain).
@@ -1218,10 +1250,18 @@ __device__ __forceinline__ bool stage_tile(const EncodeArgs& a, ConstParamPtr cp
   const uint32_t* x = cparams[c].x;
   if (tile_base + kTE > a.P || ((uintptr_t)x & 15u) || (FC_ABL & 64)) return false;
   const uint32_t j = (uint32_t)lane >> 4, q = (uint32_t)lane & 15u;
-  const uint32_t* src = x + tile_base + 16u * ((q - 4u * j) & 15u) + 4u * j;
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-    __builtin_amdgcn_global_load_lds((const void*)(src + 256 * b), (void*)(stg + 256 * b), 16, 0, 0);
+  // one lane address for all four: the instruction offset (1 KiB * b) applies to
+  // both the global and the LDS address, and the LDS base stays the staging array
+  // (typed pointers: generic ones cost a null-checked M0 and a 64-bit add per DMA)
+  typedef __attribute__((address_space(1))) void* gvptr;
+  typedef __attribute__((address_space(3))) void* lvptr;
+  const uint32_t lane_bytes = 4u * (16u * ((q - 4u * j) & 15u) + 4u * j);
+  const gvptr src = (gvptr)((const char*)(x + tile_base) + lane_bytes);
+  const lvptr dst = (lvptr)stg;
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 1024, 0);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 2048, 0);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 3072, 0);
   return true;
 }
 __device__ __forceinline__ int stage_pos(int lane, int j) {
@@ -1489,6 +1529,14 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
 
     // ---- the pending tile: look-back, publish its prefix, store its words ----
     if (pv) {
+      // the pending state is wave-uniform: readfirstlane keeps the bookkeeping
+      // below on the scalar unit (the loop-carried copies may live in VGPRs)
+      pt = (int32_t)uniform((uint32_t)pt);
+      pc = (int32_t)uniform((uint32_t)pc);
+      pfirst = (int32_t)uniform((uint32_t)pfirst);
+      plast = (int32_t)uniform((uint32_t)plast);
+      pbody = uniform(pbody);
+      ptail = uniform(ptail);
       uint32_t* win = wins[buf ^ 1];
       const int64_t tile_base = (int64_t)pt * kTE;
       const bool last_tile = (pt == a.T - 1);

@@ -18,6 +18,7 @@ MODE = int(os.environ.get("MODE", _lib.STOCHASTIC))
 STEP = float(os.environ.get("STEP", 0.5))
 SIGMAS = [float(v) for v in os.environ.get("SIGMA", "1.0").split(",")]
 REPS = int(os.environ.get("REPS", 5))
+DEC = os.environ.get("DEC", "1") != "0"
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev)
 rows = []
@@ -41,7 +42,8 @@ for SIGMA in SIGMAS:
     e[0].record(s)
     codec.quantize_encode(None, STEP, seeds, MODE, ptrs=ptrs, P=P, out=batch, stream=s)
     e[1].record(s)
-    codec.decode_accumulate(batch, want_sum=False, out=out, step=STEP, err=err, stream=s)
+    if DEC:  # DEC=0: encode only (ablation builds write streams the decoder must not be fed)
+      codec.decode_accumulate(batch, want_sum=False, out=out, step=STEP, err=err, stream=s)
     e[2].record(s)
     torch.cuda.synchronize()
     if it:
