@@ -102,8 +102,12 @@ __device__ __forceinline__ void philox10_ukey(uint32_t& c0, uint32_t& c1, uint32
     // round keys recomputed on the scalar unit at each use (volatile: not hoisted
     // across chunks, where 20 live key SGPRs would spill into VGPR lanes)
     uint32_t kk0, kk1;
-    asm volatile("s_add_u32 %0, %1, %2" : "=s"(kk0) : "s"(k0), "i"(0x9E3779B9u * (uint32_t)r));
-    asm volatile("s_add_u32 %0, %1, %2" : "=s"(kk1) : "s"(k1), "i"(0xBB67AE85u * (uint32_t)r));
+    // (readfirstlane: a no-op on the SGPR key, and a guard should the register
+    // allocator ever hand the key over in a VGPR)
+    asm volatile("s_add_u32 %0, %1, %2" : "=s"(kk0) : "s"(__builtin_amdgcn_readfirstlane(k0)),
+                 "i"(0x9E3779B9u * (uint32_t)r));
+    asm volatile("s_add_u32 %0, %1, %2" : "=s"(kk1) : "s"(__builtin_amdgcn_readfirstlane(k1)),
+                 "i"(0xBB67AE85u * (uint32_t)r));
     const uint32_t n0 = r < 2 ? (uint32_t)(p1 >> 32) ^ c1 ^ kk0 : xor3_vvs((uint32_t)(p1 >> 32), c1, kk0);
     const uint32_t n2 = r < 2 ? (uint32_t)(p0 >> 32) ^ c3 ^ kk1 : xor3_vvs((uint32_t)(p0 >> 32), c3, kk1);
     c1 = (uint32_t)p1;
@@ -274,6 +278,7 @@ struct EncodeArgs {
   uint32_t* counter2;    // exact kernel's ticket counter
   uint32_t div_m, div_l;  // ticket / nclients by multiply-high (Granlund-Montgomery)
   int32_t lb_lane0;       // first lane whose status the look-back prefetches (64 - window)
+  int32_t T2;             // super-tiles (two tiles) per client: k_encode2's tickets and statuses
 };
 
 // The launch's EncodeArgs re-read from the kernarg segment (k_encode and
@@ -396,6 +401,7 @@ __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgc
 // Decoupled look-back for tile t of one client, run by one full wave.  Returns
 // the exclusive prefix (a root segment: body = stream bits before tile t).
 // pre1/pre2 (optional): this lane's status of tile t-1-lane, loaded earlier.
+template <int SPAN = kTE>  // elements per status slot (tile, or super-tile)
 __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int lane,
                                         bool& slow, bool have_pre = false,
                                         uint64_t pre1 = 0, uint64_t pre2 = 0) {
@@ -446,7 +452,7 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
       if (tii < -1) continue;
       const uint64_t a1 = ((uint64_t)__builtin_amdgcn_readlane(w1hi, i) << 32) | __builtin_amdgcn_readlane(w1lo, i);
       const uint64_t a2 = ((uint64_t)__builtin_amdgcn_readlane(w2hi, i) << 32) | __builtin_amdgcn_readlane(w2lo, i);
-      W = seg_combine(W, seg_from_status(a1, a2, tii * kTE));
+      W = seg_combine(W, seg_from_status(a1, a2, tii * SPAN));
     }
     S = seg_combine(W, S);
     if (k < 64) break;
@@ -470,6 +476,7 @@ __device__ unsigned long long g_stamps[16];
 // otherwise the scalar lookback() does the whole fold (rare: a nearly empty
 // tile).  Out of line: it keeps its registers off the common path.
 constexpr uint32_t kSegSlow = 0xFFFFFFFFu;  // lookback_deep's "a slow tile" result (has_nz)
+template <int SPAN = kTE>
 __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, int lane,
                                           uint64_t pre1, uint64_t pre2) {
   // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
@@ -536,7 +543,7 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
     const bool agg = lane > p;
     const uint32_t fr = (h1 >> 17) & 0x1FFFu, lr = (h1 >> 4) & 0x1FFFu;
     const bool nz = agg && fr != kNoPos;
-    const int32_t tb = ti * kTE;
+    const int32_t tb = ti * SPAN;
     int32_t lastv = agg ? -1 : (lane == p ? plast : -1);
     lastv = nz ? tb + (int32_t)lr : lastv;
     const int32_t M = dpp_incl_max(lastv);
@@ -547,7 +554,7 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
     const uint32_t csum = (uint32_t)wave_sum_i((int32_t)contrib);
     if (__builtin_amdgcn_readlane(l1, 63) < 32u) {  // short newest body: exact scalar fold
       bool slow = false;
-      Seg r2 = lookback(status_c, t, lane, slow);
+      Seg r2 = lookback<SPAN>(status_c, t, lane, slow);
       if (slow) r2.has_nz = kSegSlow;
       return r2;
     }
@@ -585,9 +592,10 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
 // first run code length, and the sum of bodies.  The combined tail is the
 // newest tile's tail whenever that tile's body has >= 32 bits; otherwise the
 // scalar lookback() does the fold.  No prefix within 64 tiles: lookback_deep().
+template <int SPAN>
 __device__ __noinline__ Seg lookback_vec_wait(const uint64_t* status_c, int32_t t, int lane, uint64_t pre1,
                                               uint64_t pre2);
-template <bool WAIT>
+template <bool WAIT, int SPAN>
 __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32_t t, int lane,
                                                  bool& slow, uint64_t pre1,
                                                  uint64_t pre2) {
@@ -610,7 +618,7 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     p = pre ? 63 - (int)__clzll(pre) : 0;
     const uint64_t need = ~0ull << p;
     if (pre == 0 || (val & need) != need) {
-      Seg r = lookback_vec_wait(status_c, t, lane, pre1, pre2);
+      Seg r = lookback_vec_wait<SPAN>(status_c, t, lane, pre1, pre2);
       if (r.has_nz == kSegSlow) {
         slow = true;
         r = seg_identity();
@@ -624,7 +632,7 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     const uint64_t val = __ballot(valid);
     if (pre == 0) {  // no prefix in the window: walk 64-tile windows
       FC_COUNT(10, 1);
-      Seg r = lookback_deep(status_c, t, lane, pre1, pre2);
+      Seg r = lookback_deep<SPAN>(status_c, t, lane, pre1, pre2);
       if (r.has_nz == kSegSlow) {
         slow = true;
         r = seg_identity();
@@ -677,7 +685,7 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
   const bool agg = lane > p;
   const uint32_t fr = (h1 >> 17) & 0x1FFFu, lr = (h1 >> 4) & 0x1FFFu;
   const bool nz = agg && fr != kNoPos;
-  const int32_t tb = ti * kTE;
+  const int32_t tb = ti * SPAN;
   int32_t lastv = agg ? -1 : (lane == p ? plast : -1);
   lastv = nz ? tb + (int32_t)lr : lastv;
   const int32_t M = dpp_incl_max(lastv);
@@ -709,16 +717,18 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
 }
 
 // The waiting variant, out of line (a re-poll, or no prefix in the window).
+template <int SPAN>
 __device__ __noinline__ Seg lookback_vec_wait(const uint64_t* status_c, int32_t t, int lane, uint64_t pre1,
                                               uint64_t pre2) {
   bool slow = false;
-  Seg r = lookback_vec_impl<true>(status_c, t, lane, slow, pre1, pre2);
+  Seg r = lookback_vec_impl<true, SPAN>(status_c, t, lane, slow, pre1, pre2);
   if (slow) r.has_nz = kSegSlow;
   return r;
 }
+template <int SPAN = kTE>
 __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t, int lane, bool& slow,
                                             uint64_t pre1, uint64_t pre2) {
-  return lookback_vec_impl<false>(status_c, t, lane, slow, pre1, pre2);
+  return lookback_vec_impl<false, SPAN>(status_c, t, lane, slow, pre1, pre2);
 }
 
 // Runtime-indexed read of a small register array without scratch (select chain).
@@ -1060,10 +1070,11 @@ constexpr uint32_t kPre = 96;
 // sparse clients) all sit at the same window position -- unconditional ORs made
 // an all-zero round 2.5x slower than a dense one (81 vs 32 ms at 1024 x 25 M;
 // skipping each word a code does not reach costs 2 % more on dense data).
+template <uint32_t W = kWinWords>
 __device__ __forceinline__ void emit64(uint32_t* win, uint64_t acc, uint32_t len, uint32_t wp) {
   const uint64_t X = acc << ((64u - len) & 63u);  // MSB-aligned (len 0: acc is 0)
   const uint32_t o = wp & 31u;
-  const uint32_t i0 = min(wp >> 5, (uint32_t)kWinWords);
+  const uint32_t i0 = min(wp >> 5, W);
   const uint32_t hi = (uint32_t)(X >> 32), lo = (uint32_t)X;
   if (len) {
     atomicOr(&win[i0], hi >> o);
@@ -1073,10 +1084,11 @@ __device__ __forceinline__ void emit64(uint32_t* win, uint64_t acc, uint32_t len
 }
 
 // Same for a code of len <= 32 bits: two ds_or_b32.
+template <uint32_t W = kWinWords>
 __device__ __forceinline__ void emit32(uint32_t* win, uint32_t v, uint32_t len, uint32_t wp) {
   const uint32_t X = (uint32_t)((uint64_t)v << ((32u - len) & 63u));  // MSB-aligned (len 0: v is 0)
   const uint32_t o = wp & 31u;
-  const uint32_t i0 = min(wp >> 5, (uint32_t)kWinWords);
+  const uint32_t i0 = min(wp >> 5, W);
   if (len) {
     atomicOr(&win[i0], X >> o);
     atomicOr(&win[i0 + 1], __builtin_amdgcn_alignbit(X, 0u, o));
@@ -1641,6 +1653,321 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
   if (lane == 0)
     for (int i = 0; i < 8; ++i) atomicAdd(&g_stamps[i], (unsigned long long)st_acc[i]);
 #endif
+}
+
+// Super-tile encoder: one wave codes two consecutive tiles of one client (a
+// 2048-element super-tile) into one LDS window -- each half exactly as
+// k_encode codes a tile, the second half's lane scans continuing from the
+// first half's body and last nonzero -- and then publishes one status, runs
+// one look-back and stores the super-tile's words.  The per-ticket work that
+// does not grow with the elements (ticket, status prefetch and publish, look-back,
+// leading pieces, store and clear set-up, reductions) is paid once per 2048
+// elements.  No pending tile: the look-back window is requested when the second
+// half starts, so its round trip overlaps that half's work, and the LDS holds one
+// window of the super-tile's size instead of two.  Statuses are per super-tile
+// (slot t2 of the client's row); the decoder index stays per 1024-element tile.
+#ifndef FC_WIN2_WORDS
+#define FC_WIN2_WORDS (2 * FC_WIN_WORDS)
+#endif
+constexpr uint32_t kWin2Words = FC_WIN2_WORDS;
+constexpr int kSTE = 2 * kTE;  // elements per super-tile
+
+// LDS-DMA of one full, 16-B-aligned tile into the staging (as stage_tile).
+__device__ __forceinline__ bool stage_at(const uint32_t* x, int64_t tile_base, int64_t P, uint32_t* stg,
+                                         int lane) {
+  if (tile_base + kTE > P || ((uintptr_t)x & 15u)) return false;
+  const uint32_t j = (uint32_t)lane >> 4, q = (uint32_t)lane & 15u;
+  typedef __attribute__((address_space(1))) void* gvptr;
+  typedef __attribute__((address_space(3))) void* lvptr;
+  const uint32_t lane_bytes = 4u * (16u * ((q - 4u * j) & 15u) + 4u * j);
+  const gvptr src = (gvptr)((const char*)(x + tile_base) + lane_bytes);
+  const lvptr dst = (lvptr)stg;
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 1024, 0);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 2048, 0);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 3072, 0);
+  return true;
+}
+
+template <int MODE, bool INT_IN, int DIV, bool PRE>
+__global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode2(EncodeArgs a) {
+  __shared__ uint32_t win[kWin2Words + 3];  // + guard words
+  __shared__ uint32_t clut[kCodeLut];
+  __shared__ __attribute__((aligned(16))) uint32_t stg[kTE];  // LDS-DMA staging of the next tile
+  const int lane = threadIdx.x;
+  for (int i = lane; i < kCodeLut; i += kEncThreads) clut[i] = code_lut_entry((uint32_t)i);
+  for (int i = lane; i < (int)kWin2Words + 3; i += kEncThreads) win[i] = 0;
+  const uint32_t total = (uint32_t)a.nclients * (uint32_t)a.T2;
+  const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
+  const int64_t P = a.P;
+  const uint32_t shard = blockIdx.x % a.nshards;
+  uint32_t* my_counter = a.counter + kShardStride * shard;
+  // tickets run one ahead: the next super-tile's first tile is staged while the
+  // current one's second tile computes
+  uint32_t tk = 0;
+  if (lane == 0) tk = atomicAdd(my_counter, 1u);
+  uint32_t ticket = shard + a.nshards * uniform(tk);
+  uint32_t tk1 = 0;
+  if (ticket < total && lane == 0) tk1 = atomicAdd(my_counter, 1u);
+  uint32_t ticket1 = ticket < total ? shard + a.nshards * uniform(tk1) : ticket;
+  bool staged = false;
+  if (ticket < total) {
+    const int32_t t2 = (int32_t)div_clients(a, ticket);
+    const int32_t c = (int32_t)(ticket - (uint32_t)t2 * (uint32_t)a.nclients);
+    staged = stage_at(cparams[c].x, (int64_t)t2 * kSTE, P, stg, lane);
+  }
+  __builtin_amdgcn_s_waitcnt(kWaitVm0);
+
+  while (ticket < total) {
+    const int32_t t2 = (int32_t)div_clients(a, ticket);
+    const int32_t c = (int32_t)(ticket - (uint32_t)t2 * (uint32_t)a.nclients);
+    const int32_t t0 = 2 * t2;  // first tile of the super-tile
+    const bool has1 = t0 + 1 < a.T;
+    const int64_t sbase = (int64_t)t2 * kSTE;
+    // the client's parameters: the quantiser and row here, the stream at the end
+    // (re-read there: fewer scalar registers held across the two tiles)
+    const ClientQ cq = client_q_of(ld_param(cparams + c), PRE);
+    const uint32_t* xrow = cparams[c].x;
+    uint32_t ntk = 0;
+    uint64_t pw1 = 0, pw2 = 0;  // look-back window (lane i: super-tile t2-64+i); 0: not fetched
+    float dist = 0.0f;
+    int32_t nnz = 0;  // INT_IN: per lane; float input: wave total
+    uint32_t lng = 0;  // lane has a long chunk (either tile)
+    uint32_t body = 0, body0 = 0;
+    int32_t sfirst = -1, slast = -1, last0 = -1;  // super-tile-relative first / last nonzero
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1) {
+        if (!has1) break;
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);  // the second tile's staging has landed
+      }
+      const int64_t tile_base = sbase + (int64_t)h * kTE;
+      const bool full = tile_base + kTE <= P;
+      const int32_t lrel = 16 * lane;
+      uint32_t raw[kChunks][4];
+      if (!staged) {  // a client's last (partial) tile or an unaligned row: load into the staging
+#pragma unroll
+        for (int j = 0; j < kChunks; ++j) {
+          const int64_t e0 = tile_base + lrel + 4 * j;
+          uint4 v;
+          if (full) {
+            v = *(const uint4*)(xrow + e0);
+          } else {
+            v.x = e0 < P ? xrow[e0] : 0u;
+            v.y = e0 + 1 < P ? xrow[e0 + 1] : 0u;
+            v.z = e0 + 2 < P ? xrow[e0 + 2] : 0u;
+            v.w = e0 + 3 < P ? xrow[e0 + 3] : 0u;
+          }
+          *(uint4*)(stg + stage_pos(lane, j)) = v;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kChunks; ++j) {
+        const uint4 v = stage_read(stg, lane, j);
+        raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the staging is free once read: stage this super-tile's second tile, or the
+      // next super-tile's first (waited for before it is read)
+      if (h == 0 && has1) {
+        staged = stage_at(xrow, tile_base + kTE, P, stg, lane);
+      } else {
+        staged = false;
+        if (ticket1 < total) {
+          const int32_t n2 = (int32_t)div_clients(a, ticket1);
+          const int32_t nc = (int32_t)(ticket1 - (uint32_t)n2 * (uint32_t)a.nclients);
+          staged = stage_at(cparams[nc].x, (int64_t)n2 * kSTE, P, stg, lane);
+          // the ticket after next: its round trip completes under this tile's work
+          if (lane == 0) ntk = atomicAdd(my_counter, 1u);
+        }
+        // the look-back window, loaded under the last tile's work
+        if (t2 + lane >= 64 && lane >= a.lb_lane0) {
+          const uint64_t* sp = a.status + 2 * ((int64_t)c * a.T + t2 - 64 + lane);
+          pw1 = ld_agent(sp);
+          pw2 = ld_agent(sp + 1);
+        }
+      }
+      // ---- A: quantise + code the lane's four chunks (super-tile-relative positions)
+      int32_t lfirst = -1, llast = -1;
+      uint32_t llen = 0;
+      uint64_t cacc[kChunks];
+      uint32_t clen[kChunks];
+      const int32_t hrel = h * kTE + lrel;
+#pragma unroll
+      for (int j = 0; j < kChunks; ++j) {
+        const int32_t rel0 = hrel + 4 * j;
+        ChunkCode cc;
+        if (INT_IN) {
+          int32_t q4[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) q4[k] = (int32_t)raw[j][k];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
+          cc = chunk_local(q4, rel0);
+        } else {
+          const uint32_t g = (uint32_t)((tile_base + lrel + 4 * j) >> 2);
+          if (MODE == FC_DITHERED && !full)
+            cc = quant_code_fast<MODE, DIV, PRE, true>(cq, g, raw[j], rel0, dist, nnz, clut,
+                                                  (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - lrel - 4 * j)));
+          else
+            cc = quant_code_fast<MODE, DIV, PRE>(cq, g, raw[j], rel0, dist, nnz, clut);
+        }
+        chunk_prepend(cc, llast);  // no-op without an earlier nonzero in the lane
+        lfirst = lfirst < 0 ? cc.first : lfirst;
+        llast = cc.last >= 0 ? cc.last : llast;
+        lng |= cc.lng;
+        cacc[j] = cc.acc;
+        clen[j] = cc.len;
+        llen += cc.len;
+        FC_CHUNK_BARRIER;
+      }
+      // ---- B: scans -- last nonzero before each lane (lane 0: the first half's
+      //      last nonzero, or none), then code offsets after the bits so far
+      const int32_t im = dpp_incl_max(max(llast, slast));  // slast < every position of this tile
+      const int32_t lprev = dpp_shr1(im, slast);
+      const int32_t hlast = lane63(im);
+      const bool lrun = lfirst >= 0 && lprev >= 0;
+      const uint32_t dv = lrun ? (uint32_t)(lfirst - lprev) : 0u;
+      const uint32_t R = lrun ? glen(dv) : 0u;
+      const uint32_t ltot = R + llen;
+      const uint32_t is = dpp_incl_sum(ltot);
+      const uint32_t hbody = (uint32_t)lane63((int32_t)is);
+      // ---- C: emit the lane's run code and chunks
+      {
+        uint32_t o = kPre + body + is - ltot;
+        emit32<kWin2Words>(win, dv, R, o);
+        o += R;
+#pragma unroll
+        for (int j = 0; j < kChunks; ++j) {
+          emit64<kWin2Words>(win, cacc[j], clen[j], o);
+          o += clen[j];
+        }
+      }
+      if (sfirst < 0) {
+        const uint64_t fm = __ballot(lfirst >= 0);  // lanes are in element order
+        sfirst = fm ? __builtin_amdgcn_readlane(lfirst, (int)__builtin_ctzll(fm)) : -1;
+      }
+      slast = hlast >= 0 ? hlast : slast;
+      body += hbody;
+      if (h == 0) {
+        body0 = hbody;
+        last0 = hlast;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);  // next tile staged, look-back window loaded
+    // fast path: no long chunk, prefix + body + trailing code + one funnel word fit
+    // the window, and a finite distortion (no NaN / infinite r)
+    const float dsum = INT_IN ? 0.0f : wave_sum_f(dist);
+    const bool fast = __ballot(lng != 0) == 0 && kPre + body + 96u <= 32u * kWin2Words &&
+                      (INT_IN || dsum <= 3.4028235e38f);
+    uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t2);
+    if (fast) {
+      const float d = DIV == 1 ? dsum * (cq.step * cq.step) : dsum;  // DIV 1: sums of (sc - r)^2
+      const int32_t n = INT_IN ? wave_sum_i(nnz) : nnz;
+      if (lane == 0) {  // one partial per super-tile (its second tile's slot: 0)
+        if (a.dist_part) {
+          a.dist_part[(int64_t)c * a.T + t0] = d;
+          if (has1) a.dist_part[(int64_t)c * a.T + t0 + 1] = 0.0f;
+        }
+        if (a.nnz_part) {
+          a.nnz_part[(int64_t)c * a.T + t0] = n;
+          if (has1) a.nnz_part[(int64_t)c * a.T + t0 + 1] = 0;
+        }
+      }
+    }
+    const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;
+    Seg agg;
+    agg.has_nz = slast >= 0;
+    agg.first = agg.has_nz ? (int32_t)(sbase + sfirst) : 0;
+    agg.last = agg.has_nz ? (int32_t)(sbase + slast) : 0;
+    agg.body = body;
+    agg.tail = agg_tail;
+    bool slow = !fast;
+    Seg excl = seg_identity();
+    if (fast) {
+      if (t2 == 0) {  // chain root: the inclusive prefix right away
+        excl.has_nz = 1;
+        excl.first = excl.last = -1;
+        if (lane == 0) {
+          const Seg incl = seg_combine(excl, agg);
+          st_agent(st + 1, kFlagPre | incl.tail);
+          st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+        }
+      } else {
+        if (lane == 0) {
+          const uint64_t fr = slast >= 0 ? (uint64_t)sfirst : kNoPos;
+          const uint64_t lr = slast >= 0 ? (uint64_t)slast : kNoPos;
+          st_agent(st + 1, kFlagAgg | agg_tail);
+          st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
+        }
+        excl = lookback_vec<kSTE>(a.status + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2);
+      }
+    }
+    if (slow) {
+      // a code past the fast path's limits, a body beyond the window, or a slow
+      // predecessor: the client is re-encoded by k_encode_exact
+      if (lane == 0) {
+        st_agent(st + 1, kFlagSlow);
+        st_agent(st, kFlagSlow);
+        const EncodeArgs& ka = enc_args_fresh();
+        if (atomicOr(&ka.slow_flag[c], 1) == 0) ka.slow_list[atomicAdd(ka.slow_count, 1u)] = c;
+      }
+      for (int i = lane; i < (int)kWin2Words; i += kEncThreads) win[i] = 0;
+    } else {
+      const bool last_st = t2 == a.T2 - 1;
+      const Seg incl = seg_combine(excl, agg);
+      const uint32_t r0 = (uint32_t)(excl.body & 31);
+      const uint32_t dfirst = agg.has_nz ? (uint32_t)(agg.first - excl.last) : 0u;
+      const uint32_t R0 = agg.has_nz ? glen(dfirst) : 0u;
+      const uint32_t bstart = r0 + R0;  // stream-window bit where the body starts
+      const uint32_t tb = excl.tail & (r0 ? ((1u << r0) - 1u) : 0u);
+      uint32_t trail_len = 0;
+      uint64_t trail = 0;
+      if (last_st) {
+        const int64_t zc = P - 1 - (int64_t)incl.last;  // trailing zeros
+        if (zc > 0) {
+          trail = (uint64_t)(zc + 1);
+          trail_len = 2u * (63u - (uint32_t)__clzll(trail)) + 1u;
+        }
+      }
+      if (lane == 0) {
+        if (t2 > 0) {
+          st_agent(st + 1, kFlagPre | incl.tail);
+          st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+        }
+        const int64_t ib = (int64_t)c * (a.T + 1);
+        a.idx[ib + t0] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
+        if (has1) {  // the second tile: after the first's code (and the run code before it)
+          const uint64_t off = excl.body + (last0 >= 0 ? (uint64_t)R0 + body0 : 0u);
+          const int32_t lb = last0 >= 0 ? (int32_t)(sbase + last0) : excl.last;
+          a.idx[ib + t0 + 1] = (off & kMask36) | ((uint64_t)(lb + 1) << 36);
+        }
+        if (last_st) {
+          a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
+          enc_args_fresh().total_bits[c] = (int64_t)incl.body + trail_len;
+        }
+        // leading pieces just before the body, trailing code after it
+        emit64<kWin2Words>(win, tb, r0, kPre - bstart);
+        emit64<kWin2Words>(win, dfirst, R0, kPre - R0);
+        if (trail_len) emit64<kWin2Words>(win, trail, trail_len, kPre + body);
+      }
+      const uint32_t nwin_bits = bstart + body + trail_len;
+      const uint32_t nwords_owned = last_st ? (nwin_bits + 31) / 32 : nwin_bits / 32;
+      const ClientParam cp = ld_param(cparams + c);
+      const int64_t cap = cp.cap;
+      uint32_t* out32 = cp.out;
+      const uint64_t w0 = excl.body >> 5;
+      if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&enc_args_fresh().overflow[c], 1u);
+      const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
+      for (uint32_t k = lane; k < nwords_owned; k += kEncThreads) {
+        const uint32_t wv32 = win_bits32(win, s0 + 32 * k);
+        if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
+      }
+      const uint32_t nt = min(kWin2Words, (kPre + body + trail_len + 31) / 32 + 1);
+      for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
+    }
+    ticket = ticket1;
+    if (ticket1 < total) ticket1 = shard + a.nshards * uniform(ntk);
+  }
 }
 
 // Reset the look-back status (and overflow flag) of the clients k_encode
@@ -2881,6 +3208,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   a.nclients = nclients;
   a.P = P;
   a.T = (int32_t)T;
+  a.T2 = (int32_t)((T + 1) / 2);
   a.step = step;
   a.norms = norms;
   a.prescale = int_in ? nullptr : prescale;
@@ -2921,9 +3249,11 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
                     (sbits & 0x7FFFFFu) != 0x7FFFFFu;
   a.rcp = (pow2 || mark) ? 1.0f / step : 0.0f;
   void (*kern)(EncodeArgs) = nullptr;
+  void (*kern2)(EncodeArgs) = nullptr;
   void (*exact)(EncodeArgs) = nullptr;
   const bool pre = !int_in && prescale != nullptr;
-#define FC_PICK(M, I, D, Q) (kern = k_encode<M, I, D, Q>, exact = k_encode_exact<M, I, D == 1>)
+#define FC_PICK(M, I, D, Q) \
+  (kern = k_encode<M, I, D, Q>, kern2 = k_encode2<M, I, D, Q>, exact = k_encode_exact<M, I, D == 1>)
 #define FC_PICK2(M, D) (pre ? FC_PICK(M, false, D, true) : FC_PICK(M, false, D, false))
 #define FC_PICK3(M) (pow2 ? FC_PICK2(M, 1) : mark ? FC_PICK2(M, 2) : FC_PICK2(M, 0))
   if (int_in) FC_PICK(FC_UNIFORM, true, 0, false);
@@ -2941,6 +3271,17 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
     a.div_m = l == 0 ? 0u : (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
   }
   if ((uint64_t)nclients * (uint64_t)T >= (1ull << 32)) return fail(-1, "too many tiles (nclients x tiles >= 2^32)");
+  // Super-tiles (k_encode2) when few tiles of a client are in flight (many clients):
+  // their look-back runs right after the super-tile's own aggregate, so with many
+  // super-tiles of one client in flight it waits on predecessors still coding
+  // (1024 x 25 M: 39.0 vs 40.8 ms; 512 x 25 M: 21.8 vs 21.2; 128 x 25 M: 10.4 vs 6.2)
+  int per_cu0 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu0, kern2, kEncThreads, 0) != hipSuccess || per_cu0 < 1)
+    per_cu0 = 1;
+  bool super = (int64_t)ncu * per_cu0 <= 4LL * nclients && T >= 2;
+  if (const char* e = getenv("FEDCODEC_ENC2")) super = atoi(e) != 0;  // test knob
+  if (super) kern = kern2;
+  const int64_t tickets = super ? (int64_t)nclients * a.T2 : total;
   // Persistent grid no larger than what is co-resident (every ticket stream has a
   // running workgroup); very few clients: cap the tiles in flight per client (about
   // 256) so a look-back walks at most a few 64-tile windows.
@@ -2949,7 +3290,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
     per_cu = 1;
   int64_t max_grid = std::min<int64_t>((int64_t)ncu * per_cu, std::max<int64_t>(128, 128LL * nclients));
   if (const char* g = getenv("FEDCODEC_ENC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
-  const int grid = (int)std::min<int64_t>(total, max_grid);
+  const int grid = (int)std::min<int64_t>(tickets, max_grid);
   a.nshards = (uint32_t)std::min(kTicketShards, grid);
   {  // look-back prefetch window: 64 statuses when few tiles of a client are in flight,
      // 16 when many are (measured at 25 M: C = 128 -13 %, C = 1024 +2 % with 16)
