@@ -2167,7 +2167,7 @@ __device__ __noinline__ CodeVal slow_code(const uint8_t* base, int64_t cap, uint
 // together every kDecBatch iterations, so the wave's in-order memory counter
 // does not make a lane wait for loads other lanes issued an iteration ago.
 #ifndef FC_DEC_ABL
-#define FC_DEC_ABL 0  // decoder ablation bits (diagnostics only): 1 sums one bank per lane, 2 no sums, 4 table reads one bank per lane
+#define FC_DEC_ABL 0  // decoder ablation bits (diagnostics only): 1 sums one bank per lane, 2 no sums, 8 eight clients' streams for all lanes
 #endif
 #ifndef FC_DEC_BATCH
 #define FC_DEC_BATCH 4
@@ -2183,10 +2183,6 @@ constexpr int kDecChunk = FC_DEC_CHUNK;  // 16-byte blocks per chunk (one 64-B l
 #ifndef FC_DEC_LONG_LANES
 #define FC_DEC_LONG_LANES 16  // waiting lanes that trigger an arithmetic slot before its turn
 #endif
-#ifndef FC_DEC_STEPS
-#define FC_DEC_STEPS 2
-#endif
-constexpr int kDecSteps = FC_DEC_STEPS;  // table steps per iteration (2 always fit the window)
 constexpr int kDecLong = FC_DEC_LONG;  // iterations between arithmetic-decode slots (power of 2)
 struct SegReader {
   const uint4* p;
@@ -2236,7 +2232,8 @@ struct SegReader {
     if (rb == 0) take_block();
     return w;
   }
-  __device__ __forceinline__ void init(const uint8_t* base, int64_t cap, uint64_t bit) {
+  // left: segment bits from `bit` on -- window bits past the segment end are zeroed
+  __device__ __forceinline__ void init(const uint8_t* base, int64_t cap, uint64_t bit, int32_t left) {
     p = (const uint4*)base + ((bit >> 7) & ~(uint64_t)(kDecChunk - 1));  // chunk-aligned
     end = (const uint4*)base + (cap >> 4);
     nv = 0;
@@ -2248,6 +2245,7 @@ struct SegReader {
     const int skip = (int)(bit & 31);
     win <<= skip;
     nwin = 64 - skip;
+    if (left < nwin) win = left > 0 ? win & (~0ull << (64 - left)) : 0ull;
     batch();
   }
 };
@@ -2319,10 +2317,10 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
                                                uint64_t b1, int32_t rel, uint32_t my_addr,
                                                const uint32_t* lut, int32_t* err, float scale) {
   SegReader r;
-  r.init(base, cap, b0);
+  const int32_t total = (int32_t)(b1 - b0);
+  r.init(base, cap, b0, total);
   // one running count of consumed bits: the segment end and the window refill
   // compare against it (fill = cons + valid window bits)
-  const int32_t total = (int32_t)(b1 - b0);
   int32_t cons = 0;
   int32_t fill = r.nwin;
   uint32_t relb = my_addr + 4u * (uint32_t)rel;  // byte address of the previous nonzero's slot
@@ -2333,16 +2331,10 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     if ((++it & (kDecBatch - 1)) == 0) r.batch();  // every active lane is on the same iteration
     uint32_t moved = 0;
 #pragma unroll
-    for (int st = 0; st < kDecSteps; ++st) {  // table steps (the window holds >= 32 bits)
-#if FC_DEC_ABL & 4  // diagnostics: conflict-free table reads (every lane its own bank; wrong codes)
-      uint32_t e = lut[((uint32_t)(r.win >> 58) << 6) | (threadIdx.x & 63u)];
-#else
-      uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
-#endif
-      // codes past the segment end belong to the client's next tile: such an entry is dropped
-      // (from the third step on, so is one reaching past the window's valid bits)
-      const int32_t lim = st < 2 ? total - cons : min(total - cons, fill - cons);
-      e = (e >> 26) <= (uint32_t)lim ? e : 0u;
+    for (int st = 0; st < 2; ++st) {  // table steps (the window holds >= 33 bits when they start)
+      // the window is zero past the segment end (the client's next tile): no table
+      // entry takes a code there
+      const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
       relb += e & 0x7Fu;
       acc_add_at<FACC>(relb, ((int32_t)(e << 12)) >> 26, scale);
       relb += (e >> 7) & 0x7Fu;
@@ -2352,16 +2344,15 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       cons += (int32_t)L;
       if (st == 0) moved = L;  // a zero first step leaves the window as it was: so does the second
     }
-    // A lane whose table steps took nothing (a code longer than 12 bits, or a code
-    // pair running past the segment end) decodes one code arithmetically -- only on
-    // every kDecLong-th iteration, so the wave runs that block rarely instead of
-    // whenever any of its 64 lanes needs it; the lane idles meanwhile.
-    // (or at once when a quarter of the wave is waiting: streams of long codes,
-    // e.g. 8-bit steps, would otherwise decode one code every kDecLong iterations)
+    // A lane whose table steps took nothing (a code longer than 12 bits) decodes one
+    // code arithmetically -- only on every kDecLong-th iteration, so the wave runs
+    // that block rarely instead of whenever any of its 64 lanes needs it; the lane
+    // idles meanwhile.  (Or at once when a quarter of the wave is waiting: streams
+    // of long codes, e.g. 8-bit steps, would otherwise decode one code every
+    // kDecLong iterations.)
     const bool idle = moved == 0;
     if (idle && ((it & (kDecLong - 1)) == 0 || __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES)) {
-      // right after a refill (>= 33 window bits): one code decoded arithmetically --
-      // near the segment end, or a code longer than 12 bits
+      // right after a refill (>= 33 window bits): one code decoded arithmetically
       const uint32_t top = (uint32_t)(r.win >> 32);
       const uint32_t z1 = (uint32_t)__clz(top);
       const uint32_t sa = 30u - 2u * z1;        // sign-bit position
@@ -2383,7 +2374,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
         L = cv.L;
         d = cv.d;
         v = cv.v;
-        r.init(base, cap, pos + L);
+        r.init(base, cap, pos + L, total - cons - (int32_t)L);
         fill = cons + (int32_t)L + r.nwin;
       }
       // the run may come from far before the tile: bound it before scaling to bytes
@@ -2395,7 +2386,10 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       cons += (int32_t)L;
     }
     if (fill - cons <= 32) {
-      r.win |= (uint64_t)r.pop32() << (32 - (fill - cons));
+      uint32_t w = r.pop32();
+      const int32_t rem = total - fill;  // segment bits in this word (>= 32 but near the end)
+      if (rem < 32) w = rem > 0 ? w & (~0u << (32 - rem)) : 0u;
+      r.win |= (uint64_t)w << (32 - (fill - cons));
       fill += 32;
     }
   }
@@ -2430,12 +2424,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_DEC
     if (t < a.t_end) {
       const int64_t tile_base = t * kTE;
       for (int c = l; c < a.nclients; c += a.lanes_per_tile) {
-        const int64_t ib = (int64_t)c * (a.T + 1) + t;
+#if FC_DEC_ABL & 8  // diagnostics: 8 clients' streams and indexes for every lane (cache-resident reads)
+        const int cc = c & 7;
+#else
+        const int cc = c;
+#endif
+        const int64_t ib = (int64_t)cc * (a.T + 1) + t;
         const uint64_t e0 = a.idx[ib], e1 = a.idx[ib + 1];
         const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
         if (bend <= bstart) continue;
         const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
-        decode_segment<FACC>(a.stream_buf + a.stream_off[c], a.stream_cap[c], bstart, bend, rel, my_addr, lut, a.err,
+        decode_segment<FACC>(a.stream_buf + a.stream_off[cc], a.stream_cap[cc], bstart, bend, rel, my_addr, lut, a.err,
                               FACC ? a.client_scale[c] : 0.0f);
       }
     }
