@@ -843,11 +843,11 @@ __device__ __forceinline__ float div_step(float x, float step, float y) {
   return x / step;
 }
 
-template <int MODE, int DIV, bool PRE, bool MASK = false>
+template <int MODE, int DIV, bool PRE, bool MASK = false, bool PAIR = false>
 __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t g,
                                                      const uint32_t (&r4)[4], int32_t rel0,
                                                      float& dist, int32_t& nnz, const uint32_t* clut,
-                                                     int32_t nvalid = 4) {
+                                                     int32_t nvalid = 4, const uint32_t* plut = nullptr) {
   uint4 rb = make_uint4(0, 0, 0, 0);
   if (FC_ABL & 8) {  // diagnostics: a cheap hash instead of Philox
     rb.x = g * 2654435761u; rb.y = rb.x ^ 0x9E3779B9u; rb.z = rb.x + cq.key.k0; rb.w = rb.y ^ cq.key.k1;
@@ -883,6 +883,45 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
     nz[k] = r != 0.0f;
     nnz += (int32_t)__popcll(__ballot(nz[k]));  // wave total, scalar unit
   }
+  // the chunk's first / last nonzero, as selects here, before the code paths
+  // branch (computed after them the compiler turned the chains into branches)
+  int32_t cfirst = nz[0] ? rel0 : (nz[1] ? rel0 + 1 : (nz[2] ? rel0 + 2 : (nz[3] ? rel0 + 3 : -1)));
+  int32_t clast = nz[3] ? rel0 + 3 : (nz[2] ? rel0 + 2 : (nz[1] ? rel0 + 1 : (nz[0] ? rel0 : -1)));
+  asm volatile("" : "+v"(cfirst), "+v"(clast));
+  ChunkCode r;
+  r.acc = 0;
+  r.len = 0;
+  if (FC_ABL & 128) {  // diagnostics: no code construction (stand-in codes, wrong stream)
+    r.acc = __float_as_uint(q[0]) ^ __float_as_uint(q[1]) ^ __float_as_uint(q[2]) ^ __float_as_uint(q[3]);
+    r.len = 12;
+    r.first = rel0;
+    r.last = rel0 + 3;
+    r.lng = 0;
+    return r;
+  }
+  // max |r| of the chunk: two v_max3_f32 with |.| source modifiers.  A NaN may
+  // drop out of the max, but a NaN or infinite r always makes the distortion
+  // non-finite, which k_encode checks per tile before trusting the fast path.
+  const float mabs = vmax3_abs(q[0], q[1], vmax3_abs(q[2], q[3], 0.0f));
+  const bool bad = !(mabs < 8192.0f);
+  // small values across the wave (|q| <= 31, the common case): one table read per element
+  const bool big = !(mabs <= 31.0f);
+  if (PAIR && __ballot(!(mabs <= 7.0f)) == 0) {
+    // |q| <= 7 across the wave: one pair-table read per two elements.  Byte offset
+    // 4 * ((qb & 15) << 4 | (qa & 15)): q * 4 (q * 64) + 1.5 * 2^23 is exact and its
+    // low bits are 4q mod 64 (64q mod 1024); the second pair's table region is the
+    // run state the first pair's entry hands on (bits 31:30 -> byte offset 1024 s)
+    const uint32_t a0 = __float_as_uint(fmaf(q[0], 4.0f, 12582912.0f));
+    const uint32_t b0 = __float_as_uint(fmaf(q[1], 64.0f, 12582912.0f));
+    const uint32_t e0 = *(const uint32_t*)((const char*)plut + ((a0 & 0x3Cu) | (b0 & 0x3C0u)));
+    const uint32_t a1 = __float_as_uint(fmaf(q[2], 4.0f, 12582912.0f));
+    const uint32_t b1 = __float_as_uint(fmaf(q[3], 64.0f, 12582912.0f));
+    const uint32_t e1 =
+        *(const uint32_t*)((const char*)plut + ((a1 & 0x3Cu) | (b1 & 0x3C0u) | ((e0 >> 20) & 0xC00u)));
+    const uint32_t l1 = (e1 >> 18) & 31u;
+    r.acc = ((uint64_t)(e0 & 0x3FFFFu) << l1) | (e1 & 0x3FFFFu);
+    r.len = ((e0 >> 18) & 31u) + l1;
+  } else {
   // run code (value dv in rl bits) before element k, from the previous nonzero in the chunk
   const uint32_t dv1 = nz[0] ? 1u : 0u;
   const uint32_t dv2 = nz[1] ? 1u : (nz[0] ? 2u : 0u);
@@ -891,16 +930,6 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
   const uint32_t rl3 = nz[2] ? 1u : ((nz[1] || nz[0]) ? 3u : 0u);
   const uint32_t dv[4] = {0u, dv1, dv2, dv3};
   const uint32_t rl[4] = {0u, dv1, rl2, rl3};
-  ChunkCode r;
-  r.acc = 0;
-  r.len = 0;
-  // max |r| of the chunk: two v_max3_f32 with |.| source modifiers.  A NaN may
-  // drop out of the max, but a NaN or infinite r always makes the distortion
-  // non-finite, which k_encode checks per tile before trusting the fast path.
-  const float mabs = vmax3_abs(q[0], q[1], vmax3_abs(q[2], q[3], 0.0f));
-  const bool bad = !(mabs < 8192.0f);
-  // small values across the wave (|q| <= 31, the common case): one table read per element
-  const bool big = !(mabs <= 31.0f);
   if (__ballot(big) == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -927,8 +956,9 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
     r.len += L;
   }
   }
-  r.first = nz[0] ? rel0 : (nz[1] ? rel0 + 1 : (nz[2] ? rel0 + 2 : (nz[3] ? rel0 + 3 : -1)));
-  r.last = nz[3] ? rel0 + 3 : (nz[2] ? rel0 + 2 : (nz[1] ? rel0 + 1 : (nz[0] ? rel0 : -1)));
+  }
+  r.first = cfirst;
+  r.last = clast;
   r.lng = (bad || r.len > 64u) ? 1u : 0u;
   return r;
 }
@@ -949,6 +979,41 @@ __device__ __forceinline__ uint32_t code_lut_entry(uint32_t i) {
     L += glen(ds);
   }
   return code | (L << 16);
+}
+
+// Pair table (k_encode2): entry (s << 8) | ((qb & 15) << 4) | (qa & 15) for two
+// consecutive elements qa, qb with |q| <= 7 and run state s -- the distance from
+// the chunk's last nonzero before the pair to qa (0: none; the pair's first
+// nonzero is then the chunk's first, whose run code is prepended later) --
+// holds [17:0] the pair's code, [22:18] its length, [31:30] the state for the
+// next pair (1 if qb is nonzero, 2 if only qa is, else 0).
+constexpr int kPairLut = 768;
+__device__ __forceinline__ uint32_t pair_lut_entry(uint32_t i) {
+  const uint32_t s = i >> 8;
+  const int32_t qa = ((int32_t)(i << 28)) >> 28, qb = ((int32_t)(i << 24)) >> 28;
+  if (qa < -7 || qb < -7) return 0u;  // |q| = 8: never looked up
+  uint32_t code = 0, len = 0;
+  const int32_t qs[2] = {qa, qb};
+  uint32_t run = s;  // distance from the last nonzero to the next element (0: none)
+  for (int k = 0; k < 2; ++k) {
+    const int32_t q = qs[k];
+    if (q != 0) {
+      const uint32_t m = (uint32_t)(q < 0 ? -q : q);
+      const uint32_t ml = glen(m);
+      uint32_t c = ((uint32_t)(q > 0) << ml) | m, L = 1u + ml;
+      if (run) {
+        c |= run << L;
+        L += glen(run);
+      }
+      code = (code << L) | c;
+      len += L;
+      run = 1;
+    } else if (run) {
+      ++run;
+    }
+  }
+  const uint32_t snext = qb != 0 ? 1u : (qa != 0 ? 2u : 0u);
+  return code | (len << 18) | (snext << 30);
 }
 
 // Prepend the run code of the chunk's first nonzero once the last nonzero
@@ -1689,18 +1754,31 @@ __device__ __forceinline__ bool stage_at(const uint32_t* x, int64_t tile_base, i
   return true;
 }
 
+// Four independent waves per workgroup: they share the code tables (LDS per wave
+// = window + staging + a quarter of the tables), nothing else -- each takes its
+// own tickets; the only barrier is after the tables are built.
+constexpr int kEnc2Waves = 4;
+#ifndef FC_PAIR_LUT
+#define FC_PAIR_LUT 1
+#endif
 template <int MODE, bool INT_IN, int DIV, bool PRE>
-__global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode2(EncodeArgs a) {
-  __shared__ uint32_t win[kWin2Words + 3];  // + guard words
+__global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_encode2(EncodeArgs a) {
+  __shared__ uint32_t wins[kEnc2Waves][kWin2Words + 3];  // + guard words
   __shared__ uint32_t clut[kCodeLut];
-  __shared__ __attribute__((aligned(16))) uint32_t stg[kTE];  // LDS-DMA staging of the next tile
-  const int lane = threadIdx.x;
-  for (int i = lane; i < kCodeLut; i += kEncThreads) clut[i] = code_lut_entry((uint32_t)i);
+  __shared__ uint32_t plut[kPairLut];
+  __shared__ __attribute__((aligned(16))) uint32_t stgs[kEnc2Waves][kTE];  // LDS-DMA staging of the next tile
+  for (int i = threadIdx.x; i < kCodeLut; i += kEncThreads * kEnc2Waves) clut[i] = code_lut_entry((uint32_t)i);
+  for (int i = threadIdx.x; i < kPairLut; i += kEncThreads * kEnc2Waves) plut[i] = pair_lut_entry((uint32_t)i);
+  const int wave = (int)uniform(threadIdx.x >> 6);  // wave-uniform (the compiler cannot tell)
+  const int lane = (int)(threadIdx.x & 63u);
+  uint32_t* win = wins[wave];
+  uint32_t* stg = stgs[wave];
   for (int i = lane; i < (int)kWin2Words + 3; i += kEncThreads) win[i] = 0;
+  __syncthreads();
   const uint32_t total = (uint32_t)a.nclients * (uint32_t)a.T2;
   const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
   const int64_t P = a.P;
-  const uint32_t shard = blockIdx.x % a.nshards;
+  const uint32_t shard = (blockIdx.x * kEnc2Waves + (uint32_t)wave) % a.nshards;
   uint32_t* my_counter = a.counter + kShardStride * shard;
   // tickets run one ahead: the next super-tile's first tile is staged while the
   // current one's second tile computes
@@ -1806,10 +1884,11 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode2(EncodeArg
         } else {
           const uint32_t g = (uint32_t)((tile_base + lrel + 4 * j) >> 2);
           if (MODE == FC_DITHERED && !full)
-            cc = quant_code_fast<MODE, DIV, PRE, true>(cq, g, raw[j], rel0, dist, nnz, clut,
-                                                  (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - lrel - 4 * j)));
+            cc = quant_code_fast<MODE, DIV, PRE, true, FC_PAIR_LUT>(
+                cq, g, raw[j], rel0, dist, nnz, clut,
+                (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - lrel - 4 * j)), plut);
           else
-            cc = quant_code_fast<MODE, DIV, PRE>(cq, g, raw[j], rel0, dist, nnz, clut);
+            cc = quant_code_fast<MODE, DIV, PRE, false, FC_PAIR_LUT>(cq, g, raw[j], rel0, dist, nnz, clut, 4, plut);
         }
         chunk_prepend(cc, llast);  // no-op without an earlier nonzero in the lane
         lfirst = lfirst < 0 ? cc.first : lfirst;
@@ -3275,21 +3354,23 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   // super-tiles of one client in flight it waits on predecessors still coding
   // (1024 x 25 M: 39.0 vs 40.8 ms; 512 x 25 M: 21.8 vs 21.2; 128 x 25 M: 10.4 vs 6.2)
   int per_cu0 = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu0, kern2, kEncThreads, 0) != hipSuccess || per_cu0 < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu0, kern2, kEncThreads * kEnc2Waves, 0) != hipSuccess ||
+      per_cu0 < 1)
     per_cu0 = 1;
-  bool super = (int64_t)ncu * per_cu0 <= 4LL * nclients && T >= 2;
+  bool super = (int64_t)ncu * per_cu0 * kEnc2Waves <= 4LL * nclients && T >= 2;
   if (const char* e = getenv("FEDCODEC_ENC2")) super = atoi(e) != 0;  // test knob
   if (super) kern = kern2;
+  const int wpg = super ? kEnc2Waves : 1;  // waves per workgroup
   const int64_t tickets = super ? (int64_t)nclients * a.T2 : total;
   // Persistent grid no larger than what is co-resident (every ticket stream has a
-  // running workgroup); very few clients: cap the tiles in flight per client (about
+  // running wave); very few clients: cap the tiles in flight per client (about
   // 256) so a look-back walks at most a few 64-tile windows.
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kEncThreads, 0) != hipSuccess || per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kEncThreads * wpg, 0) != hipSuccess || per_cu < 1)
     per_cu = 1;
-  int64_t max_grid = std::min<int64_t>((int64_t)ncu * per_cu, std::max<int64_t>(128, 128LL * nclients));
+  int64_t max_grid = std::min<int64_t>((int64_t)ncu * per_cu * wpg, std::max<int64_t>(128, 128LL * nclients));
   if (const char* g = getenv("FEDCODEC_ENC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
-  const int grid = (int)std::min<int64_t>(tickets, max_grid);
+  const int grid = (int)std::min<int64_t>(tickets, max_grid);  // waves
   a.nshards = (uint32_t)std::min(kTicketShards, grid);
   {  // look-back prefetch window: 64 statuses when few tiles of a client are in flight,
      // 16 when many are (measured at 25 M: C = 128 -13 %, C = 1024 +2 % with 16)
@@ -3301,7 +3382,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   hipLaunchKernelGGL(k_client_params, dim3((nclients + 255) / 256), dim3(256), 0, s, a,
                      (ClientParam*)a.cparams, (int)(!int_in && mode != FC_UNIFORM));
   if (hipGetLastError() != hipSuccess) return fail(-10, "k_client_params launch");
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kEncThreads), 0, s, a);
+  hipLaunchKernelGGL(kern, dim3((grid + wpg - 1) / wpg), dim3(kEncThreads * wpg), 0, s, a);
   if (hipGetLastError() != hipSuccess) return check_launch("k_encode");
   // clients with a tile beyond the fast path: exact re-encode (no-ops otherwise)
   hipLaunchKernelGGL(k_zero_slow, dim3(256), dim3(256), 0, s, a);
