@@ -2263,6 +2263,15 @@ constexpr int kDecChunk = FC_DEC_CHUNK;  // 16-byte blocks per chunk (one 64-B l
 #define FC_DEC_LONG_LANES 16  // waiting lanes that trigger an arithmetic slot before its turn
 #endif
 constexpr int kDecLong = FC_DEC_LONG;  // iterations between arithmetic-decode slots (power of 2)
+// Batch-point loads as inline asm the compiler's wait-count pass does not see:
+// a lane taking its next block would otherwise wait (in-order vmcnt) for the
+// loads the whole wave issued at the latest batch point.  A batch point first
+// waits for the previous one's loads (issued kDecBatch iterations earlier), so a
+// block requested there is known to have landed ("ready") from then on.
+#ifndef FC_DEC_ASYNC
+#define FC_DEC_ASYNC 1
+#endif
+constexpr bool kDecAsync = FC_DEC_ASYNC && kDecChunk == 1;
 struct SegReader {
   const uint4* p;
   const uint4* end;
@@ -2270,8 +2279,19 @@ struct SegReader {
   uint4 nxt[kDecChunk];                          // next chunk (requested)
   int32_t cb;                                    // blocks left in cur
   uint32_t nv;                                   // nxt holds a chunk not yet taken
+  uint32_t rdy;                                  // (async) that chunk has landed
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 anx;                                     // (async) the next block, one register tuple
   uint64_t win, rh, rl;
   int32_t nwin, rb;
+  __device__ __forceinline__ void wait_nxt() {  // every outstanding load of the wave has landed
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(anx) :: "memory");
+  }
+  __device__ __forceinline__ void load_async() {
+    const uint4* q = p < end ? p : end - 1;  // clamped
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(anx) : "v"(q) : "memory");
+    p += 1;
+  }
   __device__ __forceinline__ void load_chunk(uint4* dst) {
 #pragma unroll
     for (int i = 0; i < kDecChunk; ++i) dst[i] = *(p + i < end ? p + i : end - 1);  // clamped
@@ -2290,6 +2310,18 @@ struct SegReader {
       --cb;
       return;
     }
+    if (kDecAsync) {
+      if (!nv) {  // segment start, restart after a long code, or a lane far ahead
+        load_async();
+        wait_nxt();
+      } else if (!rdy) {
+        wait_nxt();  // requested at the latest batch point
+      }
+      nv = 0;
+      rdy = 0;
+      set_res(make_uint4(anx.x, anx.y, anx.z, anx.w));
+      return;
+    }
     if (!nv) load_chunk(nxt);  // segment start, restart after a long code, or a lane far ahead
     nv = 0;
     set_res(nxt[0]);
@@ -2298,6 +2330,15 @@ struct SegReader {
     cb = kDecChunk - 1;
   }
   __device__ __forceinline__ void batch() {
+    if (kDecAsync) {
+      wait_nxt();  // the previous batch point's loads
+      rdy = nv;
+      if (!nv) {
+        load_async();
+        nv = 1;
+      }
+      return;
+    }
     if (!nv) {
       load_chunk(nxt);
       nv = 1;
@@ -2316,6 +2357,7 @@ struct SegReader {
     p = (const uint4*)base + ((bit >> 7) & ~(uint64_t)(kDecChunk - 1));  // chunk-aligned
     end = (const uint4*)base + (cap >> 4);
     nv = 0;
+    rdy = 0;
     cb = 0;
     take_block();
     for (int i = (int)((bit >> 5) & (4 * kDecChunk - 1)); i > 0; --i) (void)pop32();
