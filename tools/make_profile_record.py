@@ -23,6 +23,7 @@ from collections import defaultdict
 
 KERNELS = {  # name fragment -> (key, FETCH multiplier)
     "::k_encode<": ("k_encode", 2.0),
+    "::k_encode2<": ("k_encode", 2.0),  # the super-tile variant (same LDS-DMA staging)
     "k_decode<": ("k_decode", 1.0),
     "k_client_norms": ("k_client_norms", 2.0),
     "k_mask_encode<": ("k_mask_encode", 2.0),
