@@ -1020,10 +1020,11 @@ __device__ __forceinline__ uint32_t pair_lut_entry(uint32_t i) {
 // before the chunk (prev, tile-relative, -1 = none in this tile) is known.
 __device__ __forceinline__ void chunk_prepend(ChunkCode& r, int32_t prev) {
   if (r.first >= 0 && prev >= 0) {
-    const uint32_t d = (uint32_t)(r.first - prev);
-    const uint32_t rl = 2u * (31u - __clz(d)) + 1u;
+    const uint32_t d = (uint32_t)(r.first - prev);           // >= 1
+    const uint32_t rl = 63u - 2u * (uint32_t)__builtin_clz(d);  // glen(d)
+    // past 64 bits the chunk is long: the tile takes the exact path, acc is then unused
     r.lng |= (r.len + rl > 64u) ? 1u : 0u;
-    r.acc = (r.len + rl > 64u) ? 0 : (((uint64_t)d << r.len) | r.acc);
+    r.acc |= (uint64_t)d << (r.len & 63u);
     r.len += rl;
   }
 }
@@ -1870,6 +1871,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       uint64_t cacc[kChunks];
       uint32_t clen[kChunks];
       const int32_t hrel = h * kTE + lrel;
+      const uint32_t gbase = (uint32_t)(tile_base >> 2) + 4u * (uint32_t)lane;  // Philox counter of chunk 0
 #pragma unroll
       for (int j = 0; j < kChunks; ++j) {
         const int32_t rel0 = hrel + 4 * j;
@@ -1882,7 +1884,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
           cc = chunk_local(q4, rel0);
         } else {
-          const uint32_t g = (uint32_t)((tile_base + lrel + 4 * j) >> 2);
+          const uint32_t g = gbase + (uint32_t)j;
           if (MODE == FC_DITHERED && !full)
             cc = quant_code_fast<MODE, DIV, PRE, true, FC_PAIR_LUT>(
                 cq, g, raw[j], rel0, dist, nnz, clut,
@@ -1915,10 +1917,18 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         uint32_t o = kPre + body + is - ltot;
         emit32<kWin2Words>(win, dv, R, o);
         o += R;
+        if (__ballot(clen[0] + clen[1] > 64u || clen[2] + clen[3] > 64u) == 0) {
+          // chunk pairs fit 64 bits across the wave (the common case): two pieces, not four
+          const uint64_t a01 = (cacc[0] << (clen[1] & 63u)) | cacc[1];
+          const uint64_t a23 = (cacc[2] << (clen[3] & 63u)) | cacc[3];
+          emit64<kWin2Words>(win, a01, clen[0] + clen[1], o);
+          emit64<kWin2Words>(win, a23, clen[2] + clen[3], o + clen[0] + clen[1]);
+        } else {
 #pragma unroll
-        for (int j = 0; j < kChunks; ++j) {
-          emit64<kWin2Words>(win, cacc[j], clen[j], o);
-          o += clen[j];
+          for (int j = 0; j < kChunks; ++j) {
+            emit64<kWin2Words>(win, cacc[j], clen[j], o);
+            o += clen[j];
+          }
         }
       }
       if (sfirst < 0) {
