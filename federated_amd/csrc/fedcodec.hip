@@ -2459,6 +2459,12 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
   uint32_t bad = 0;
   uint32_t it = 0;
   while (cons < total) {
+#ifdef FC_STAMPS
+    {  // diagnostics (tools/diag/dec_diverge.py): wave iterations, one count per iteration the wave runs
+      const uint64_t ex = __ballot(1);
+      if ((uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(ex)) atomicAdd(&g_stamps[15], 1ull);
+    }
+#endif
     if ((++it & (kDecBatch - 1)) == 0) r.batch();  // every active lane is on the same iteration
     uint32_t moved = 0;
 #pragma unroll
@@ -2527,6 +2533,9 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
   // every decoded value must have landed inside this tile's accumulator
   bad |= (relb < lo_addr || relb >= hi_addr) ? 1u : 0u;
   if (bad || cons != total) atomicOr(err, 1);
+#ifdef FC_STAMPS
+  atomicAdd(&g_stamps[14], (unsigned long long)it);  // diagnostics: lane iterations
+#endif
 }
 
 // Persistent: each workgroup builds the decode table once, then walks tiles
