@@ -13,16 +13,16 @@ Mirrors ``compressed_communication/aggregators/comparison_methods/qsgd.py``
 What runs where: the per-client L2 norms (``fc_client_norms``, float64
 accumulation), then ONE fused HIP quantise + encode launch over the batch with
 a per-client step, then ONE decode launch that dequantises each client with its
-step and sums in float32 (``fc_decode_accumulate_scaled``).  The per-client
+step and sums in float32 in client order (``fc_decode_accumulate_scaled``).  The per-client
 step ``norm / num_steps`` is divided on the host in float32 (IEEE), so the
 quantiser sees exactly the step TF would compute from the same norm.
 
 Parity: q and the bitstream are bit-exact against the oracle given the norm;
 the norm itself is TF's float32 reduction in an unspecified order (here a
-correctly rounded float64 sum), and the server's float32 sum over clients is
-order-dependent (its order, and so its last bits, may also vary from run to
-run: the decoder adds the clients it decodes side by side with LDS float
-atomics), so both are compared within a tolerance.
+correctly rounded float64 sum, as the oracle's).  The server sum adds the
+clients in client order in float32 exactly as the reference's accumulate does
+(the decoder writes each client group's q rows, ``k_sum_planes`` adds them in
+order), so with the oracle's norm it is bit-exact and deterministic.
 """
 import collections
 

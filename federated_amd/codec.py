@@ -229,8 +229,10 @@ def decode_accumulate(batch, sum_in=None, want_sum=True, out=None, step=1.0, noi
   return (sum_out if want_sum else None), out, err
 
 
-def decode_accumulate_scaled(batch, client_scale, out=None, fsum_in=None, stream=None, err=None):
-  """QSGD server sum: out = [fsum_in +] sum_c float(q_c) * client_scale[c] (float32).
+def decode_accumulate_scaled(batch, client_scale, out=None, fsum_in=None, stream=None, err=None,
+                             workspace=None):
+  """QSGD server sum: out = (fsum_in or 0) + float(q_c) * client_scale[c], added in
+  client order in float32 (the reference's sequential sum, bit for bit).
 
   Returns (out, err tensor).
   """
@@ -242,10 +244,13 @@ def decode_accumulate_scaled(batch, client_scale, out=None, fsum_in=None, stream
     err = torch.zeros(1, dtype=torch.int32, device=device)
   client_scale = torch.as_tensor(client_scale, dtype=torch.float32).to(device).contiguous()
   assert client_scale.numel() == batch.nclients
+  if workspace is None:
+    nbytes = int(_lib.load().fc_decode_scaled_workspace_bytes(int(batch.nclients), int(batch.P)))
+    workspace = torch.empty(nbytes, dtype=torch.uint8, device=device)
   _lib.call("fc_decode_accumulate_scaled", _lib.ptr(batch.stream), _lib.ptr(batch.stream_off),
             _lib.ptr(batch.stream_cap), _lib.ptr(batch.idx), batch.nclients, batch.P,
             _lib.ptr(client_scale), _lib.ptr(fsum_in), _lib.ptr(out), _lib.ptr(err),
-            _lib.stream_handle(stream))
+            _lib.ptr(workspace), workspace.numel(), _lib.stream_handle(stream))
   return out, err
 
 

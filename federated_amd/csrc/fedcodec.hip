@@ -2191,8 +2191,8 @@ struct DecodeArgs {
   float step;
   const float* noise_sum;
   int32_t* err;
-  const float* client_scale;  // FACC: per-client dequantisation step
-  const float* fsum_in;       // FACC: optional float partial sum to add
+  int32_t* plane;             // PLANE: q of each client, row c at plane + c * plane_stride
+  int64_t plane_stride;
   int32_t t_begin, t_end;     // tiles decoded: [t_begin, t_end)
 };
 
@@ -2294,6 +2294,7 @@ struct SegReader {
   u32x4 anx;                                     // (async) the next block, one register tuple
   uint64_t win, rh, rl;
   int32_t nwin, rb;
+  int32_t vb;  // segment bits from the start of the next block taken (masks the last block)
   __device__ __forceinline__ void wait_nxt() {  // every outstanding load of the wave has landed
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(anx) :: "memory");
   }
@@ -2311,6 +2312,15 @@ struct SegReader {
     rh = ((uint64_t)bswap32(blk.x) << 32) | bswap32(blk.y);
     rl = ((uint64_t)bswap32(blk.z) << 32) | bswap32(blk.w);
     rb = 128;
+    if (vb < 128) {  // the segment's last block (or one past it): zero the bits after its end
+      if (vb <= 64) {
+        rh = vb > 0 ? rh & (~0ull << (64 - vb)) : 0ull;
+        rl = 0;
+      } else {
+        rl &= ~0ull << (128 - vb);
+      }
+    }
+    vb -= 128;
   }
   __device__ __forceinline__ void take_block() {
     if (kDecChunk > 1 && cb > 0) {
@@ -2366,6 +2376,7 @@ struct SegReader {
   __device__ __forceinline__ void init(const uint8_t* base, int64_t cap, uint64_t bit, int32_t left) {
     p = (const uint4*)base + ((bit >> 7) & ~(uint64_t)(kDecChunk - 1));  // chunk-aligned
     end = (const uint4*)base + (cap >> 4);
+    vb = (int32_t)(bit - ((bit >> 7) & ~(uint64_t)(kDecChunk - 1)) * 128) + max(left, 0);
     nv = 0;
     rdy = 0;
     cb = 0;
@@ -2376,7 +2387,6 @@ struct SegReader {
     const int skip = (int)(bit & 31);
     win <<= skip;
     nwin = 64 - skip;
-    if (left < nwin) win = left > 0 ? win & (~0ull << (64 - left)) : 0ull;
     batch();
   }
 };
@@ -2411,17 +2421,18 @@ __device__ __forceinline__ uint32_t lut_entry(uint32_t i) {
   return used ? (e | (used << 26)) : 0u;
 }
 
-typedef __attribute__((address_space(3))) int32_t* lds_iptr;
-typedef __attribute__((address_space(3))) float* lds_fptr;
+constexpr int kDecThreads = 256;
 
-// Accumulator add at LDS byte address a: int32 client sum, or (QSGD) the
-// float32 sum of each client's dequantised value f32(v) * scale.
-template <bool FACC>
-__device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, float scale) {
-  // (a no-op zero add may point outside the accumulator -- harmless for int32;
-  // skipped for float, where it could quiet a NaN bit pattern of a table word)
-  if (FACC) {
-    if (v != 0) atomicAdd((float*)(lds_fptr)(uintptr_t)a, (float)v * scale);
+typedef __attribute__((address_space(3))) int32_t* lds_iptr;
+
+// Accumulator add at LDS byte address a (int32 client sum), or (PLANE, the
+// QSGD server sum) a store of the value into the client's q row at byte offset a
+// of the tile -- only nonzero values (a no-op zero add may repeat the previous
+// code's slot or point past the tile) inside the tile's valid bytes `hib`.
+template <bool PLANE>
+__device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, int32_t* ptile, uint32_t hib) {
+  if (PLANE) {
+    if (v != 0 && a < hib) ptile[a >> 2] = v;
   } else {
 #if FC_DEC_ABL & 1
     a = (a & ~127u) | ((threadIdx.x & 31u) << 2);  // diagnostics: every lane its own bank
@@ -2443,10 +2454,11 @@ __device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, float scale) {
 // window bits in the next arithmetic slot (longer than 32 bits: slow_code, then
 // the reader restarts).  The window holds >= 33 valid bits when an iteration
 // starts.
-template <bool FACC>
+template <bool PLANE>
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
                                                uint64_t b1, int32_t rel, uint32_t my_addr,
-                                               const uint32_t* lut, int32_t* err, float scale) {
+                                               const uint32_t* lut, int32_t* err, int32_t* ptile,
+                                               uint32_t hib) {
   SegReader r;
   const int32_t total = (int32_t)(b1 - b0);
   r.init(base, cap, b0, total);
@@ -2466,6 +2478,26 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     }
 #endif
     if ((++it & (kDecBatch - 1)) == 0) r.batch();  // every active lane is on the same iteration
+#if FC_DEC_ABL & 16  // diagnostics: 12 extra independent VALU per iteration (is the loop issue-bound?)
+    {
+      uint32_t p0 = it, p1 = it + 1, p2 = it + 2, p3 = it + 3;
+      asm volatile(
+          "v_add_u32 %0, %0, %4\n v_add_u32 %1, %1, %4\n v_add_u32 %2, %2, %4\n v_add_u32 %3, %3, %4\n"
+          "v_add_u32 %0, %0, %4\n v_add_u32 %1, %1, %4\n v_add_u32 %2, %2, %4\n v_add_u32 %3, %3, %4\n"
+          "v_add_u32 %0, %0, %4\n v_add_u32 %1, %1, %4\n v_add_u32 %2, %2, %4\n v_add_u32 %3, %3, %4\n"
+          : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3) : "v"(relb));
+    }
+#endif
+#if FC_DEC_ABL & 32  // diagnostics: 12 extra SALU per iteration
+    {
+      uint32_t s0 = __builtin_amdgcn_readfirstlane(it), s1 = s0 + 1;
+      asm volatile(
+          "s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5\n s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5\n"
+          "s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5\n s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5\n"
+          "s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5\n s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5\n"
+          : "+s"(s0), "+s"(s1) :: "scc");
+    }
+#endif
     uint32_t moved = 0;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {  // table steps (the window holds >= 33 bits when they start)
@@ -2473,9 +2505,9 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       // entry takes a code there
       const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
       relb += e & 0x7Fu;
-      acc_add_at<FACC>(relb, ((int32_t)(e << 12)) >> 26, scale);
+      acc_add_at<PLANE>(relb, ((int32_t)(e << 12)) >> 26, ptile, hib);
       relb += (e >> 7) & 0x7Fu;
-      acc_add_at<FACC>(relb, ((int32_t)(e << 6)) >> 26, scale);
+      acc_add_at<PLANE>(relb, ((int32_t)(e << 6)) >> 26, ptile, hib);
       const uint32_t L = e >> 26;
       r.win <<= L;
       cons += (int32_t)L;
@@ -2519,13 +2551,11 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       const uint32_t rel_new = (uint32_t)(rel_now + (int32_t)d);
       bad |= rel_new >= (uint32_t)kTE ? 1u : 0u;
       relb = my_addr + 4u * min(rel_new, (uint32_t)kTE - 1);
-      acc_add_at<FACC>(relb, v, scale);
+      acc_add_at<PLANE>(relb, v, ptile, hib);
       cons += (int32_t)L;
     }
-    if (fill - cons <= 32) {
-      uint32_t w = r.pop32();
-      const int32_t rem = total - fill;  // segment bits in this word (>= 32 but near the end)
-      if (rem < 32) w = rem > 0 ? w & (~0u << (32 - rem)) : 0u;
+    if (fill - cons <= 32) {  // (the blocks are zero past the segment end)
+      const uint32_t w = r.pop32();
       r.win |= (uint64_t)w << (32 - (fill - cons));
       fill += 32;
     }
@@ -2540,26 +2570,31 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 
 // Persistent: each workgroup builds the decode table once, then walks tiles
 // (tiles_per_wg at a time) with one lane per client segment, accumulating the
-// clients' values in LDS and writing the tile's sum / dequantised values.
-template <bool FACC>
+// clients' values in LDS and writing the tile's sum / dequantised values -- or
+// (PLANE) storing each client's values into its q row (zeroed beforehand), for
+// k_sum_planes to add in client order.
+template <bool PLANE>
 #ifndef FC_DEC_WPE
 #define FC_DEC_WPE 5  // waves per SIMD the register budget is held to
 #endif
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_DEC_WPE))) void k_decode(DecodeArgs a) {
+__global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(FC_DEC_WPE))) void k_decode(DecodeArgs a) {
   __shared__ uint32_t lut[kLutSize];  // static: table reads fold its base into the offset
   extern __shared__ int32_t acc[];     // [tiles_per_wg][kTE] sums
   const int tid = threadIdx.x;
-  const int tiles_per_wg = kThreads / a.lanes_per_tile;
-  for (int i = tid; i < kLutSize; i += kThreads) lut[i] = lut_entry((uint32_t)i);
+  const int tiles_per_wg = kDecThreads / a.lanes_per_tile;
+  for (int i = tid; i < kLutSize; i += kDecThreads) lut[i] = lut_entry((uint32_t)i);
   const int sub = tid / a.lanes_per_tile;
   const int l = tid - sub * a.lanes_per_tile;
-  const uint32_t my_addr = (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * kTE);
+  const uint32_t my_addr = PLANE ? 0u : (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * kTE);
   const int64_t ngroups = (a.t_end - a.t_begin + tiles_per_wg - 1) / tiles_per_wg;
   const int64_t e_end = min(a.P, (int64_t)a.t_end * kTE);  // elements this launch writes
+  if (PLANE) __syncthreads();  // the table (the accumulator path's first barrier covers it otherwise)
   for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int64_t t0 = a.t_begin + grp * tiles_per_wg;
-    for (int i = tid; i < tiles_per_wg * kTE; i += kThreads) acc[i] = 0;
-    __syncthreads();
+    if (!PLANE) {
+      for (int i = tid; i < tiles_per_wg * kTE; i += kDecThreads) acc[i] = 0;
+      __syncthreads();
+    }
     const int64_t t = t0 + sub;
     if (t < a.t_end) {
       const int64_t tile_base = t * kTE;
@@ -2574,20 +2609,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_DEC
         const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
         if (bend <= bstart) continue;
         const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
-        decode_segment<FACC>(a.stream_buf + a.stream_off[cc], a.stream_cap[cc], bstart, bend, rel, my_addr, lut, a.err,
-                              FACC ? a.client_scale[c] : 0.0f);
+        int32_t* ptile = PLANE ? a.plane + (int64_t)c * a.plane_stride + tile_base : nullptr;
+        const uint32_t hib = PLANE ? 4u * (uint32_t)min<int64_t>(kTE, a.P - tile_base) : 0u;
+        decode_segment<PLANE>(a.stream_buf + a.stream_off[cc], a.stream_cap[cc], bstart, bend, rel, my_addr, lut, a.err,
+                              ptile, hib);
       }
     }
+    if (PLANE) continue;
     __syncthreads();
-    for (int i = tid; i < tiles_per_wg * kTE; i += kThreads) {
+    for (int i = tid; i < tiles_per_wg * kTE; i += kDecThreads) {
       const int64_t e = t0 * kTE + i;
       if (e >= e_end) break;
-      if (FACC) {  // float32 sum of dequantised clients (+ a float partial sum)
-        float f = __int_as_float(acc[i]);
-        if (a.fsum_in) f = a.fsum_in[e] + f;
-        a.out[e] = f;
-        continue;
-      }
       int32_t v = acc[i];
       if (a.sum_in) v = (int32_t)((uint32_t)v + (uint32_t)a.sum_in[e]);
       if (a.sum_out) a.sum_out[e] = v;
@@ -2630,6 +2662,30 @@ __global__ void k_dequantize(const int32_t* __restrict__ s, int64_t P, float ste
   float f = (float)s[i];
   if (noise_sum) f = f + noise_sum[i];
   out[i] = f * step;
+}
+
+// QSGD server sum (qsgd.py:88-100): acc = in (or 0), then acc = acc + f32(q_c) *
+// scale[c] for the clients of the plane rows in client order, float32 with no
+// contraction -- the reference's sequential client-order sum, bit for bit.  One
+// thread per 4 elements (rows padded to a multiple of 4 elements).
+__global__ __launch_bounds__(256) void k_sum_planes(const int32_t* __restrict__ planes, int64_t stride, int32_t n,
+                                                    int64_t P, const float* __restrict__ scale,
+                                                    const float* in, float* out) {
+  const int64_t e0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (e0 >= P) return;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int m = (int)min<int64_t>(4, P - e0);
+  if (in)
+    for (int k = 0; k < m; ++k) acc[k] = in[e0 + k];
+  for (int c = 0; c < n; ++c) {
+    const int4 q = *(const int4*)(planes + (int64_t)c * stride + e0);
+    const float sc = scale[c];
+    acc[0] = acc[0] + (float)q.x * sc;
+    acc[1] = acc[1] + (float)q.y * sc;
+    acc[2] = acc[2] + (float)q.z * sc;
+    acc[3] = acc[3] + (float)q.w * sc;
+  }
+  for (int k = 0; k < m; ++k) out[e0 + k] = acc[k];
 }
 
 // noise_sum[i] = sum over clients, in client order, of TF's dither noise
@@ -3451,7 +3507,10 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   return check_launch("k_encode_exact");
 }
 
-// Shared launcher of k_decode (int32 client sum, or float sum of scaled clients).
+// QSGD decode: client q rows per group at most this many bytes (fc_decode_scaled_workspace_bytes).
+constexpr int64_t kScaledPlaneBudget = 1LL << 30;
+
+// Shared launcher of k_decode (int32 client sum, or the q rows of a client group).
 int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap,
                   const uint64_t* idx, int32_t nclients, int64_t P, int32_t* err, void* stream,
                   int64_t tile_begin = 0, int64_t tile_end = -1, bool reset_err = true) {
@@ -3479,14 +3538,14 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
     if (v == 64 || v == 128 || v == 256) lpt = v;
   }
   a.lanes_per_tile = lpt;
-  const bool facc = a.client_scale != nullptr;
-  void (*kern)(DecodeArgs) = facc ? k_decode<true> : k_decode<false>;
-  const int tpw = kThreads / lpt;
-  const size_t lds = (size_t)tpw * kTE * sizeof(int32_t);  // + the static kLutSize-word table
+  const bool plane = a.plane != nullptr;
+  void (*kern)(DecodeArgs) = plane ? k_decode<true> : k_decode<false>;
+  const int tpw = kDecThreads / lpt;
+  const size_t lds = plane ? 0 : (size_t)tpw * kTE * sizeof(int32_t);  // + the static kLutSize-word table
   int dev = 0, ncu = 256, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds) != hipSuccess || per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kDecThreads, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
   const int64_t ngroups = (a.t_end - a.t_begin + tpw - 1) / tpw;
   // 5 workgroups/CU: more waves only add L2 line thrash (measured 4.2 ms at 5/CU vs 5.0 at 7/CU)
@@ -3495,7 +3554,7 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   const dim3 grid((unsigned)std::min<int64_t>(ngroups, max_grid));
   hipStream_t s = (hipStream_t)stream;
   if (reset_err && hipMemsetAsync(err, 0, sizeof(int32_t), s) != hipSuccess) return fail(-10, "memset err");
-  hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, s, a);
+  hipLaunchKernelGGL(kern, grid, dim3(kDecThreads), lds, s, a);
   return check_launch("k_decode");
 }
 
@@ -3585,16 +3644,44 @@ int fc_decode_accumulate_tiles(const uint8_t* stream_buf, const int64_t* stream_
                        tile_end, false);
 }
 
+int64_t fc_decode_scaled_workspace_bytes(int32_t nclients, int64_t P) {
+  if (nclients <= 0 || P <= 0) return 256;
+  const int64_t row = 4 * ((P + 3) & ~(int64_t)3);
+  const int64_t group = std::max<int64_t>(1, std::min<int64_t>(nclients, kScaledPlaneBudget / row));
+  return group * row;
+}
+
 int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream_off,
                                 const int64_t* stream_cap, const uint64_t* idx, int32_t nclients, int64_t P,
                                 const float* client_scale, const float* fsum_in, float* out, int32_t* err,
-                                void* stream) {
-  if (!out || !client_scale) return fail(-1, "null required pointer");
-  DecodeArgs a{};
-  a.out = out;
-  a.client_scale = client_scale;
-  a.fsum_in = fsum_in;
-  return decode_common(a, stream_buf, stream_off, stream_cap, idx, nclients, P, err, stream);
+                                void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!out || !client_scale || !workspace) return fail(-1, "null required pointer");
+  if (nclients <= 0) return fail(-1, "nclients must be > 0");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
+  if ((uintptr_t)workspace & 15u) return fail(-1, "workspace must be 16-byte aligned");
+  const int64_t stride = (P + 3) & ~(int64_t)3;
+  const int64_t group = std::min<int64_t>(nclients, workspace_bytes / (4 * stride));
+  if (group < 1) return fail(-1, "workspace smaller than one client row (fc_decode_scaled_workspace_bytes)");
+  const int64_t T = tiles_for(P);
+  hipStream_t s = (hipStream_t)stream;
+  // client groups in order: decode each group's q rows, then add them to the running
+  // float32 sum in client order (the first group starts from fsum_in, or zero)
+  for (int64_t c0 = 0; c0 < nclients; c0 += group) {
+    const int32_t n = (int32_t)std::min<int64_t>(group, nclients - c0);
+    if (hipMemsetAsync(workspace, 0, (size_t)n * 4 * stride, s) != hipSuccess) return fail(-10, "memset planes");
+    DecodeArgs a{};
+    a.plane = (int32_t*)workspace;
+    a.plane_stride = stride;
+    const int rc = decode_common(a, stream_buf, stream_off + c0, stream_cap + c0, idx + c0 * (T + 1), n, P, err,
+                                 stream, 0, -1, c0 == 0);
+    if (rc) return rc;
+    const int64_t thr = (P + 3) / 4;
+    hipLaunchKernelGGL(k_sum_planes, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, (const int32_t*)workspace,
+                       stride, n, P, client_scale + c0, c0 == 0 ? fsum_in : out, out);
+    const int rs = check_launch("k_sum_planes");
+    if (rs) return rs;
+  }
+  return 0;
 }
 
 int64_t fc_vote_workspace_bytes(int32_t nclients, int64_t P, int32_t K) {

@@ -142,15 +142,18 @@ int fc_decode_accumulate_tiles(const uint8_t* stream_buf, const int64_t* stream_
                                const int32_t* sum_in, int32_t* sum_out, float* out, float step,
                                const float* noise_sum, int32_t* err, void* stream);
 
-/* QSGD server side: out[i] = [fsum_in[i] +] sum over clients of
- * float(q_c[i]) * client_scale[c] in float32.  The summation order is
- * unspecified and may differ run to run (LDS float atomics over the clients
- * decoded side by side), so the last bits of out may too; the reference's
- * client-order float sum is matched within a tolerance. */
+/* QSGD server side (qsgd.py:85-112 sum_encoded_value): acc = fsum_in[i] (or 0),
+ * then acc = acc + float(q_c[i]) * client_scale[c] for c = 0 .. nclients-1 in
+ * order, float32 -- the reference's client-order sum, deterministic and bit for
+ * bit.  The clients are decoded in groups into int32 q rows in `workspace`
+ * (16-byte aligned; fc_decode_scaled_workspace_bytes gives the size for groups of
+ * up to 1 GiB of rows, at least one client row is required). */
+int64_t fc_decode_scaled_workspace_bytes(int32_t nclients, int64_t P);
 int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream_off,
                                 const int64_t* stream_cap, const uint64_t* idx, int32_t nclients,
                                 int64_t P, const float* client_scale, const float* fsum_in,
-                                float* out, int32_t* err, void* stream);
+                                float* out, int32_t* err, void* workspace, int64_t workspace_bytes,
+                                void* stream);
 
 /* Step-size vote: for each client c and option k (steps = device float[K]),
  * bits[c*K + k] = exact run-length-gamma code length (bits) of quantizing x_c

@@ -218,7 +218,7 @@ def test_qsgd_reference_execution(gpu, values, num_steps, want, bitrate):
   from federated_amd.aggregators.comparison_methods import qsgd  # pylint: disable=g-import-not-at-top
   process = qsgd.QSGDFactory(num_steps).create((np.float32, (len(values[0]),)))
   out = process.next(process.initialize(), [np.asarray(v, np.float32) for v in values])
-  np.testing.assert_allclose(out.result, want, rtol=1e-6)
+  np.testing.assert_array_equal(out.result, np.asarray(want, np.float32))
   assert out.measurements["avg_bitrate"] == np.float64(bitrate)
   assert out.measurements["avg_distortion"] == 0.0 and out.measurements["avg_sparsity"] == 0.0
 
@@ -232,17 +232,35 @@ def test_qsgd_matches_oracle(gpu, P, C):
   process = qsgd.QSGDFactory(127.0).create((np.float32, (P,)))
   out = process.next(process.initialize(), xs, seeds=seeds)
   want, m, codes = oagg.qsgd_next(xs, 127.0, seeds=seeds)
-  # q and the codes are exact given the norm; the server sum is a float32 sum over
-  # clients in an unspecified order: |err| <= C ulp-scale of the largest term
-  scale = max(np.max(np.abs(w)) for w in [want]) + 1e-30
-  np.testing.assert_allclose(out.result, want, rtol=1e-6 * C, atol=1e-6 * C * scale)
+  # the norm (correctly rounded float64 sum on both sides), q, the codes and the
+  # client-order float32 server sum are all exact
+  np.testing.assert_array_equal(out.result, want)
   assert out.measurements["avg_bitrate"] == m["avg_bitrate"]
   assert out.measurements["avg_sparsity"] == m["avg_sparsity"]
   np.testing.assert_allclose(out.measurements["avg_distortion"], m["avg_distortion"], rtol=1e-5)
-  # the float32 client sum uses LDS float atomics: its order -- and so
-  # its last bits -- may vary run to run; the variation stays within the same bound
+  # deterministic run to run (round 1 summed with LDS float atomics)
   out2 = process.next(process.initialize(), xs, seeds=seeds)
-  np.testing.assert_allclose(out2.result, out.result, rtol=2e-6 * C, atol=2e-6 * C * scale)
+  np.testing.assert_array_equal(out2.result, out.result)
+
+
+@pytest.mark.parametrize("P,C,group", [(4099, 5, 2), (2048, 300, 7), (1025, 3, 3)])
+def test_decode_scaled_client_order(gpu, P, C, group):
+  """fc_decode_accumulate_scaled in client groups (a workspace of `group` rows):
+  acc = fsum_in, then acc + f32(q_c) * s_c in client order, bit for bit."""
+  rng = np.random.default_rng(P * 7 + C)
+  qs = [rng.integers(-40, 41, P).astype(np.int32) * (rng.random(P) < 0.6) for _ in range(C)]
+  qs[0][: P // 3] = 0  # long zero runs
+  batch = codec.rlgamma_encode([torch.from_numpy(q.astype(np.int32)).to(gpu) for q in qs])
+  scale = (rng.random(C) * 3 + 1e-3).astype(np.float32)
+  fin = rng.standard_normal(P).astype(np.float32)
+  stride = (P + 3) // 4 * 4
+  ws = torch.empty(group * stride * 4, dtype=torch.uint8, device=gpu)
+  out, err = codec.decode_accumulate_scaled(batch, scale, fsum_in=torch.from_numpy(fin).to(gpu), workspace=ws)
+  assert int(err.item()) == 0
+  acc = fin.copy()
+  for c in range(C):
+    acc = (acc + (qs[c].astype(np.float32) * scale[c]).astype(np.float32)).astype(np.float32)
+  np.testing.assert_array_equal(out.cpu().numpy(), acc)
 
 
 def test_qsgd_codes_bit_exact(gpu):
