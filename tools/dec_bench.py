@@ -1,4 +1,6 @@
-"""Diagnostic: time k_decode alone on C clients x P (encode once, decode N times)."""
+"""Diagnostic: time k_decode alone on C clients x P (encode once, decode N times).
+
+C, P, STEP (0.5), SIGMA (1.0), ITERS from the environment."""
 import os
 import sys
 import time
@@ -10,19 +12,21 @@ from federated_amd import _lib, codec  # noqa: E402
 
 P = int(os.environ.get("P", 25_000_000))
 C = int(os.environ.get("C", 128))
+STEP = float(os.environ.get("STEP", 0.5))
+SIGMA = float(os.environ.get("SIGMA", 1.0))
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev)
 g.manual_seed(1)
-pool = [torch.randn(P, generator=g, device=dev) for _ in range(4)]
+pool = [torch.randn(P, generator=g, device=dev) * SIGMA for _ in range(4)]
 rows = [pool[c % 4] for c in range(C)]
 ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
 seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
-batch = codec.EncodedBatch(P, C, [P + 1024] * C, dev)
-codec.quantize_encode(None, 0.5, seeds, _lib.STOCHASTIC, ptrs=ptrs, P=P, out=batch)
+batch = codec.EncodedBatch(P, C, [2 * P + 1024] * C, dev)  # 16 bits per element
+codec.quantize_encode(None, STEP, seeds, _lib.STOCHASTIC, ptrs=ptrs, P=P, out=batch)
 out = torch.empty(P, dtype=torch.float32, device=dev)
 for it in range(int(os.environ.get("ITERS", 3))):
   torch.cuda.synchronize()
   t0 = time.perf_counter()
-  codec.decode_accumulate(batch, want_sum=False, out=out, step=0.5)
+  codec.decode_accumulate(batch, want_sum=False, out=out, step=STEP)
   torch.cuda.synchronize()
   print("decode %d clients: %.2f ms" % (C, (time.perf_counter() - t0) * 1e3))
