@@ -21,10 +21,25 @@ REPS = int(os.environ.get("REPS", 5))
 DEC = os.environ.get("DEC", "1") != "0"
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev)
+# LAYOUT: sep = one allocation per client row (2 MiB-aligned bases); pack = rows back to
+# back in one buffer; skew = one buffer, rows 2 MiB-aligned plus c * SKEW bytes
+LAYOUT = os.environ.get("LAYOUT", "sep")
 rows = []
-for c in range(C):
-  g.manual_seed(77 + c)
-  rows.append(torch.randn(P, generator=g, device=dev))
+if LAYOUT == "sep":
+  for c in range(C):
+    g.manual_seed(77 + c)
+    rows.append(torch.randn(P, generator=g, device=dev))
+else:
+  skew = int(os.environ.get("SKEW", 16384)) // 4
+  pitch = P if LAYOUT == "pack" else -(-P // (1 << 19)) * (1 << 19)
+  off = [c * pitch + (skew * (c % 64) if LAYOUT == "skew" else 0) for c in range(C)]
+  big = torch.empty(off[-1] + P, device=dev)
+  for c in range(C):
+    g.manual_seed(77 + c)
+    r = big[off[c]:off[c] + P]
+    r.copy_(torch.randn(P, generator=g, device=dev))
+    rows.append(r)
+print("row bases mod 2 MiB:", sorted(set(r.data_ptr() % (1 << 21) for r in rows))[:8], flush=True)
 ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
 seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
 batch = codec.EncodedBatch(P, C, [int(P * float(os.environ.get("CAP", 1.0))) + 1024] * C, dev)
@@ -53,6 +68,6 @@ for SIGMA in SIGMAS:
   dec.sort()
   bits = float(batch.bits().sum()) / (C * P)
   ok = not len(codec.check_overflow(batch)) and int(err.item()) == 0
-  print("%-28s C=%d P=%d mode=%d step=%g sigma=%g  encode %.3f ms  decode %.3f ms  %.3f bits/elt  %s" % (
-      os.path.basename(_lib.LIB_PATH), C, P, MODE, STEP, SIGMA, enc[len(enc) // 2], dec[len(dec) // 2], bits,
+  print("%-6s %-28s C=%d P=%d mode=%d step=%g sigma=%g  encode %.3f ms  decode %.3f ms  %.3f bits/elt  %s" % (
+      LAYOUT, os.path.basename(_lib.LIB_PATH), C, P, MODE, STEP, SIGMA, enc[len(enc) // 2], dec[len(dec) // 2], bits,
       "ok" if ok else "ERROR"), flush=True)
