@@ -2273,6 +2273,10 @@ constexpr int kDecChunk = FC_DEC_CHUNK;  // 16-byte blocks per chunk (one 64-B l
 #define FC_DEC_LONG_LANES 16  // waiting lanes that trigger an arithmetic slot before its turn
 #endif
 constexpr int kDecLong = FC_DEC_LONG;  // iterations between arithmetic-decode slots (power of 2)
+#ifndef FC_DEC_LONG_BITS
+#define FC_DEC_LONG_BITS 9
+#endif
+constexpr int kDecLongBits = FC_DEC_LONG_BITS;  // segment bits per element for the arithmetic-only loop (0: never)
 // Batch-point loads as inline asm the compiler's wait-count pass does not see:
 // a lane taking its next block would otherwise wait (in-order vmcnt) for the
 // loads the whole wave issued at the latest batch point.  A batch point first
@@ -2454,7 +2458,7 @@ __device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, int32_t* ptile
 // window bits in the next arithmetic slot (longer than 32 bits: slow_code, then
 // the reader restarts).  The window holds >= 33 valid bits when an iteration
 // starts.
-template <bool PLANE>
+template <bool PLANE, bool LONG = false>
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
                                                uint64_t b1, int32_t rel, uint32_t my_addr,
                                                const uint32_t* lut, int32_t* err, int32_t* ptile,
@@ -2500,7 +2504,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 #endif
     uint32_t moved = 0;
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {  // table steps (the window holds >= 33 bits when they start)
+    for (int st = 0; st < (LONG ? 0 : 2); ++st) {  // table steps (the window holds >= 33 bits when they start)
       // the window is zero past the segment end (the client's next tile): no table
       // entry takes a code there
       const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
@@ -2519,8 +2523,14 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     // idles meanwhile.  (Or at once when a quarter of the wave is waiting: streams
     // of long codes, e.g. 8-bit steps, would otherwise decode one code every
     // kDecLong iterations.)
-    const bool idle = moved == 0;
-    if (idle && ((it & (kDecLong - 1)) == 0 || __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES)) {
+    // LONG (a wave whose segments all average kDecLongBits or more per element, e.g.
+    // 8-bit steps): no table steps, one code decoded arithmetically every iteration
+    const bool idle = LONG || moved == 0;
+    bool stop = false;
+#pragma unroll
+    for (int u = 0; u < (LONG ? 2 : 1); ++u) {  // LONG: two codes (each after a refill) per iteration
+    if (u > 0 && cons >= total) break;
+    if (idle && (LONG || (it & (kDecLong - 1)) == 0 || __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES)) {
       // right after a refill (>= 33 window bits): one code decoded arithmetically
       const uint32_t top = (uint32_t)(r.win >> 32);
       const uint32_t z1 = (uint32_t)__clz(top);
@@ -2538,6 +2548,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
         const CodeVal cv = slow_code(base, cap, pos);
         if (cv.L == 0) {
           bad = 1;
+          stop = true;
           break;
         }
         L = cv.L;
@@ -2559,6 +2570,8 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       r.win |= (uint64_t)w << (32 - (fill - cons));
       fill += 32;
     }
+    }
+    if (stop) break;
   }
   // every decoded value must have landed inside this tile's accumulator
   bad |= (relb < lo_addr || relb >= hi_addr) ? 1u : 0u;
@@ -2611,8 +2624,13 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(FC_
         const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
         int32_t* ptile = PLANE ? a.plane + (int64_t)c * a.plane_stride + tile_base : nullptr;
         const uint32_t hib = PLANE ? 4u * (uint32_t)min<int64_t>(kTE, a.P - tile_base) : 0u;
-        decode_segment<PLANE>(a.stream_buf + a.stream_off[cc], a.stream_cap[cc], bstart, bend, rel, my_addr, lut, a.err,
-                              ptile, hib);
+        // a wave whose segments are all long-code streams skips the table steps
+        if (kDecLongBits > 0 && __ballot(bend - bstart < (uint64_t)kDecLongBits * kTE) == 0)
+          decode_segment<PLANE, true>(a.stream_buf + a.stream_off[cc], a.stream_cap[cc], bstart, bend, rel, my_addr,
+                                      lut, a.err, ptile, hib);
+        else
+          decode_segment<PLANE>(a.stream_buf + a.stream_off[cc], a.stream_cap[cc], bstart, bend, rel, my_addr, lut,
+                                a.err, ptile, hib);
       }
     }
     if (PLANE) continue;
