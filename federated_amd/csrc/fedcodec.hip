@@ -2276,6 +2276,10 @@ constexpr int kDecLong = FC_DEC_LONG;  // iterations between arithmetic-decode s
 #ifndef FC_DEC_LONG_BITS
 #define FC_DEC_LONG_BITS 9
 #endif
+#ifndef FC_DEC_LONG_UNROLL
+#define FC_DEC_LONG_UNROLL 2
+#endif
+constexpr int kDecLongUnroll = FC_DEC_LONG_UNROLL;  // arithmetic decodes per iteration of that loop
 constexpr int kDecLongBits = FC_DEC_LONG_BITS;  // segment bits per element for the arithmetic-only loop (0: never)
 // Batch-point loads as inline asm the compiler's wait-count pass does not see:
 // a lane taking its next block would otherwise wait (in-order vmcnt) for the
@@ -2528,7 +2532,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     const bool idle = LONG || moved == 0;
     bool stop = false;
 #pragma unroll
-    for (int u = 0; u < (LONG ? 2 : 1); ++u) {  // LONG: two codes (each after a refill) per iteration
+    for (int u = 0; u < (LONG ? kDecLongUnroll : 1); ++u) {  // LONG: codes (each after a refill) per iteration
     if (u > 0 && cons >= total) break;
     if (idle && (LONG || (it & (kDecLong - 1)) == 0 || __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES)) {
       // right after a refill (>= 33 window bits): one code decoded arithmetically
