@@ -2410,7 +2410,10 @@ struct SegReader {
 //   [6:0] 4*d1   [13:7] 4*d2 (0: one code)   [19:14] v1   [25:20] v2 (6-bit
 //   two's complement, 0: one code)   [29:26] L = bits of the decoded codes
 //   (0: the first code is longer than 12 bits -- the entry is then all zero)
-constexpr int kLutBits = 12;
+#ifndef FC_LUT_BITS
+#define FC_LUT_BITS 12
+#endif
+constexpr int kLutBits = FC_LUT_BITS;
 constexpr int kLutSize = 1 << kLutBits;
 
 __device__ __forceinline__ uint32_t lut_entry(uint32_t i) {
@@ -2530,7 +2533,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     if (!LONG && STEP3) {
       // a third table step where the window still holds 13 or more valid bits (so
       // the refill below restores >= 33); otherwise an empty entry
-      const bool ok3 = fill - cons >= 13;
+      const bool ok3 = fill - cons >= kLutBits + 1;
       uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
       e = ok3 ? e : 0u;
       relb += e & 0x7Fu;
