@@ -38,13 +38,20 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--clients C]
        [--workload all|headline|NAME] [--dump-result PATH]
 
 N > 1: each rank decodes its clients in S tile ranges and all-reduces each range
-while the next decodes.  Rehearsal on a 1-GPU box (never used by the driver):
-FEDCODEC_BENCH_BACKEND=gloo FEDCODEC_BENCH_ONE_DEVICE=1 with --dump-result, see
-tools/rehearse_multigpu.sh.
+while the next decodes.  `python bench.py --gpus N` (no WORLD_SIZE in the
+environment) starts its N ranks itself -- `torch.distributed.run` as a child
+process, before this process touches the GPU -- and exits with the child's
+code; under a launcher (WORLD_SIZE set) WORLD_SIZE must equal --gpus.
+`--workload onebit` at N > 1 times config 5's sharded one-bit round
+(distributed.onebit_round: float32 partial sums all-reduced).  Rehearsal on a
+1-GPU box (never used by the driver): FEDCODEC_BENCH_BACKEND=gloo
+FEDCODEC_BENCH_ONE_DEVICE=1 with --dump-result, see tools/rehearse_multigpu.sh.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -88,6 +95,35 @@ def parse():
                        "headline only; NAME: that workload alone (profiling)")
   ap.add_argument("--extra-steps", type=int, default=5, help="timed steps per extra workload")
   return ap.parse_args()
+
+
+def free_port():
+  s = socket.socket()
+  s.bind(("127.0.0.1", 0))
+  port = s.getsockname()[1]
+  s.close()
+  return port
+
+
+def launcher_cmd(argv, gpus, port):
+  """The torch.distributed.run command that starts `gpus` ranks of this script."""
+  return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(int(gpus)),
+          "--master-addr", "127.0.0.1", "--master-port", str(int(port)), os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(args, environ=None):
+  """Returns "spawn" when this process must start --gpus ranks itself (no
+  launcher, --gpus > 1), else None.  Raises SystemExit when a launcher's
+  WORLD_SIZE disagrees with --gpus.  Touches nothing on the GPU."""
+  env = os.environ if environ is None else environ
+  if "WORLD_SIZE" not in env:
+    if args.gpus < 1:
+      raise SystemExit("bench.py: --gpus must be >= 1")
+    return "spawn" if args.gpus > 1 else None
+  world = int(env["WORLD_SIZE"])
+  if world != args.gpus:
+    raise SystemExit("bench.py: WORLD_SIZE=%d from the launcher but --gpus %d" % (world, args.gpus))
+  return None
 
 
 def setup_dist(args):
@@ -377,8 +413,87 @@ def run_extra(name, args, dev, stream, head_rows, head_ptrs):
   return r
 
 
+def onebit_sharded(args, rank, world, dev, stream):
+  """Config 5 on N GPUs: C clients x P one-bit SGD (one_bit_sgd.py:45-112),
+  C / N clients per rank.  A step: fc_onebit_encode of the rank's clients, the
+  client-order float32 decode-sum in `--slabs` element ranges, each range's
+  float32 sum all-reduced (RCCL) while the next is summed."""
+  import torch.distributed as dist  # pylint: disable=g-import-not-at-top
+  P, C = args.P, args.clients
+  assert C % world == 0, "clients must divide evenly over ranks"
+  Cg = C // world
+  g = torch.Generator(device=dev)
+  rows = []
+  for i in range(Cg):
+    g.manual_seed(20251015 + rank * Cg + i)  # a delta per client, seeded by its global index
+    rows.append(torch.randn(P, generator=g, device=dev, dtype=torch.float32).mul_(args.sigma))
+  ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
+  nw = (P + 31) // 32
+  masks = torch.empty(Cg * nw, dtype=torch.int32, device=dev)
+  means = torch.empty(2 * Cg, dtype=torch.float32, device=dev)
+  dist_ = torch.empty(Cg, dtype=torch.float64, device=dev)
+  out = torch.empty(P, dtype=torch.float32, device=dev)
+  h = _lib.stream_handle(stream)
+  bounds = distributed.slab_bounds(nw, args.slabs)
+
+  def step():
+    _lib.call("fc_onebit_encode", _lib.ptr(ptrs), Cg, P, 0.0, _lib.ptr(masks), _lib.ptr(means), _lib.ptr(dist_), h)
+    works = []
+    for k in range(len(bounds) - 1):
+      _lib.call("fc_onebit_decode_sum_range", _lib.ptr(masks), _lib.ptr(means), Cg, P, bounds[k], bounds[k + 1],
+                _lib.ptr(out), h)
+      lo, hi = bounds[k] * 32, min(P, bounds[k + 1] * 32)
+      works.append(dist.all_reduce(out[lo:hi], async_op=True))
+    for w in works:
+      w.wait()
+
+  for _ in range(args.warmup):
+    step()
+  torch.cuda.synchronize()
+  dist.barrier()
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    step()
+  torch.cuda.synchronize()
+  dist.barrier()
+  wall = time.perf_counter() - t0
+  if args.dump_result and rank == 0:
+    np.save(args.dump_result, out.cpu().numpy())
+  t = torch.tensor([wall], dtype=torch.float64, device=dev)
+  dist.all_reduce(t, op=dist.ReduceOp.MAX)
+  t_step = float(t.item()) / args.steps
+  tm = Timer(stream)
+  for _ in range(max(2, min(args.steps, 5))):
+    tm.phase("k_mask_encode", lambda: _lib.call("fc_onebit_encode", _lib.ptr(ptrs), Cg, P, 0.0, _lib.ptr(masks),
+                                                 _lib.ptr(means), _lib.ptr(dist_), h))
+  ms = tm.ms()
+  result = None
+  if rank == 0:
+    enc_bytes = Cg * 4.0 * P + Cg * 4.0 * nw
+    result = {
+        "metric": "device-resident encode+decode GiB/s on 25M-fp32 deltas",
+        "value": round(C * P * 4.0 / t_step / 2**30, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_step * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32 (1-bit masks)",
+        "data": "synthetic: sigma*N(0,1) fp32 deltas generated on device, a distinct delta per client",
+        "config": {"workload": "config 5: %d clients x %d fp32 deltas, one-bit SGD (threshold 0), client-order "
+                               "float32 decode-sum + RCCL float32 all-reduce" % (C, P),
+                   "clients_per_gpu": Cg, "world_size": world, "backend": dist.get_backend(),
+                   "parallelism": "client-sharded dp%d + float32 all-reduce in %d slabs" % (world, len(bounds) - 1)},
+        "roofline": roofline("k_mask_encode", enc_bytes, ms["k_mask_encode"], "none"),
+    }
+    print(json.dumps(result), flush=True)
+  dist.barrier()
+  dist.destroy_process_group()
+  return result
+
+
 def main():
   args = parse()
+  if check_world(args) == "spawn":
+    # N ranks under torch.distributed.run, started before this process touches the GPU
+    sys.exit(subprocess.call(launcher_cmd(sys.argv[1:], args.gpus, free_port())))
   rank, world = setup_dist(args)
   dev = torch.device("cuda", torch.cuda.current_device())
   stream = torch.cuda.current_stream()
@@ -388,6 +503,10 @@ def main():
   Cg = C // world
   mode = MODES[args.mode]
   single = args.workload not in ("all", "headline")
+  if world > 1 and args.workload == "onebit":
+    return onebit_sharded(args, rank, world, dev, stream)
+  if world > 1 and single:
+    raise SystemExit("bench.py: --workload %s runs on one GPU only (N > 1: headline, onebit)" % args.workload)
 
   # ---- synthetic inputs, resident in HBM before timing ----
   g = torch.Generator(device=dev)
@@ -512,7 +631,9 @@ def main():
         "config": {"workload": "%d clients x %d fp32 deltas, %s rounding step %g, run-length Elias-gamma "
                                "code, decode + int32 client sum + dequantise" % (C, P, args.mode,
                                                                                  args.step_size),
-                   "clients_per_gpu": Cg, "parallelism": "client-sharded dp%d + RCCL int32 all-reduce"
+                   "clients_per_gpu": Cg, "world_size": world,
+                   "backend": dist.get_backend() if world > 1 else None,
+                   "parallelism": "client-sharded dp%d + RCCL int32 all-reduce"
                    % world if world > 1 else "1 GPU"},
         "roofline": rl,
         "decode": {"kernel": "k_decode", "launch_ms": round(ms["k_decode"], 3),

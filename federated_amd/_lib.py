@@ -46,6 +46,7 @@ SIGNATURES = {
     "fc_drive_encode": (_INT, [_P, _I32, _I64, _INT, _P, _P, _P, _P]),
     "fc_hadamard": (_INT, [_P, _I32, _I64, _INT, _I64, _I64, _P]),
     "fc_onebit_decode_sum": (_INT, [_P, _P, _I32, _I64, _P, _P]),
+    "fc_onebit_decode_sum_range": (_INT, [_P, _P, _I32, _I64, _I64, _I64, _P, _P]),
 }
 
 _lib = None

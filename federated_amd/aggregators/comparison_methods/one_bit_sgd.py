@@ -7,16 +7,11 @@ masked means, distortion ``sum (x - decode)^2 / P`` and bitrate ``(P + 64) / P``
 (:87-112).  Masks are kept bit-packed in HBM (1 bit per element), which is the
 wire format the bitrate already assumes.
 """
-import collections
-
-import numpy as np
 import torch
 
-from federated_amd import codec
+from federated_amd import distributed
 from federated_amd import tff_compat as tc
 from federated_amd.aggregators import _values
-
-F32 = np.float32
 
 
 class OneBitSGDFactory(tc.UnweightedAggregationFactory):
@@ -33,20 +28,23 @@ class OneBitSGDFactory(tc.UnweightedAggregationFactory):
     shape = value_type.shape
     P = value_type.num_elements
 
-    def next_fn(state, value):
-      rows, vshape, host = _values.to_device_rows(value, torch.float32)
-      if vshape != shape:
-        raise ValueError("client value shape %s != %s" % (vshape, shape))
-      masks, means, dist = codec.onebit_encode(rows, self._threshold)
-      out = codec.onebit_decode_sum(masks, means, len(rows), P)
-      size = F32(P)
-      bitrate = F32((size + F32(64.0)) / size)
-      distortion = (dist.cpu().numpy().astype(np.float32) / size).astype(np.float32)
+    def next_fn(state, value, sharded=False, group=None, slabs=4):
+      """``sharded``: this process holds one rank's block of the round's clients
+      (possibly empty); the float32 partial sums are all-reduced over ``group``
+      (config 5's 8-GPU split, distributed.onebit_round) and the distortion mean
+      is global.  The multi-rank float association differs from one process's
+      client-order sum: compare with a tolerance."""
+      if sharded and len(value) == 0:
+        rows, host = [], False
+      else:
+        rows, vshape, host = _values.to_device_rows(value, torch.float32)
+        if vshape != shape:
+          raise ValueError("client value shape %s != %s" % (vshape, shape))
+      rnd = distributed.onebit_round(rows, self._threshold, group=group, P=P, slabs=slabs,
+                                     multi=bool(sharded) and distributed.is_multi(group))
       return tc.MeasuredProcessOutput(
           state=state,
-          result=_values.finish(out, shape, host),
-          measurements=collections.OrderedDict(
-              avg_bitrate=bitrate,
-              avg_distortion=F32(np.mean(distortion, dtype=np.float32))))
+          result=_values.finish(rnd.result, shape, host),
+          measurements=rnd.measurements)
 
     return tc.AggregationProcess(lambda: (), next_fn)

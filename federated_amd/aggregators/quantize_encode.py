@@ -30,6 +30,7 @@ import torch
 
 from federated_amd import _lib
 from federated_amd import codec
+from federated_amd import distributed
 from federated_amd import tff_compat as tc
 from federated_amd.aggregators import _values
 from federated_amd.aggregators.utils import quantize_utils
@@ -108,10 +109,23 @@ class QuantizeEncodeFactory(tc.UnweightedAggregationFactory):
           step_size=F32(factory._step_size),
           inner_state=())
 
-    def next_fn(state, value, seeds=None, prescale=None):
-      rows, vshape, host = _values.to_device_rows(value, torch.float32)
-      if vshape != shape:
-        raise ValueError("client value shape %s != %s" % (vshape, shape))
+    # host-side process memory (not TFF state): the previous round's code sizes
+    # size this round's stream capacities (codec.CapacityHint)
+    cap_hint = codec.CapacityHint()
+
+    def next_fn(state, value, seeds=None, prescale=None, sharded=False, group=None):
+      """``sharded``: this process holds one rank's block of the round's clients
+      (``value``, ``seeds`` and ``prescale`` are that block's, possibly empty);
+      the int32 sums and the measurements are reduced over ``group`` (default:
+      the torch.distributed world; distributed.aggregate_round) and every rank
+      returns the round's global result.  The state is replicated: every rank
+      steps it the same way."""
+      if sharded and len(value) == 0:
+        rows, host = [], False
+      else:
+        rows, vshape, host = _values.to_device_rows(value, torch.float32)
+        if vshape != shape:
+          raise ValueError("client value shape %s != %s" % (vshape, shape))
       C = len(rows)
       step_size = F32(state["step_size"])
       if seeds is None:
@@ -122,38 +136,24 @@ class QuantizeEncodeFactory(tc.UnweightedAggregationFactory):
       # normalize_fn sees the value behind the clipping / mean wrappers (:145): the
       # norm of the pre-scaled elements, as the encoder quantises them
       norms = (codec.client_norms(rows, factory._norm_kind, prescale=prescale)
-               if factory._norm_kind else None)
-      batch = codec.quantize_encode_checked(rows, step_size, seeds, factory._mode, norms=norms,
-                                            prescale=prescale)
-      noise_sum = codec.noise_sum(seeds, P, rows[0].device) if factory._mode == _lib.DITHERED else None
-      out = torch.empty(P, dtype=torch.float32, device=rows[0].device)
-      # the server dequantises with the un-normalised state step (quantize_encode.py:189-190)
-      _, out, err = codec.decode_accumulate(batch, want_sum=False, out=out, step=float(step_size),
-                                            noise_sum=noise_sum)
-      dist, nnz = codec.finalize(batch)
-      if int(err.item()):
-        raise RuntimeError("malformed run-length gamma code")
-      # measurements (quantize_encode.py:150-155, 184-185; elias_gamma_encode.py:100-108)
-      size = F32(P)
-      distortion = (dist.cpu().numpy().astype(np.float32) / size).astype(np.float32)
-      nz = nnz.cpu().numpy().astype(np.float32)
-      sparsity = ((size - nz) / size).astype(np.float32)
-      nbits = batch.bits()
-      bitstring_lengths = 8.0 * ((nbits + 7) // 8).astype(np.float64)
-      avg_len = np.mean(bitstring_lengths)
-      avg_bitrate = np.float64(avg_len / np.float64(P)) if P else np.float64(0.0)
+               if factory._norm_kind and C else None)
+      # encode (quantize :139-156 + tfc encode), decode + int32 sum, dequantise with
+      # the un-normalised state step (:189-190), measurements (:150-155, 184-185;
+      # elias_gamma_encode.py:100-108)
+      rnd = distributed.aggregate_round(rows, step_size, seeds, factory._mode, group=group, prescale=prescale,
+                                        norms=norms, caps=cap_hint.caps(P, C), P=P,
+                                        multi=bool(sharded) and distributed.is_multi(group))
+      if rnd.batch is not None:
+        cap_hint.update(rnd.batch)
       next_round = F32(state["round_num"] + F32(1.0))
       next_state = collections.OrderedDict(
           round_num=next_round,
           step_size=F32(factory._schedule_fn(next_round)),
           inner_state=state["inner_state"])
-      measurements = collections.OrderedDict(
-          avg_bitrate=avg_bitrate,
-          avg_distortion=F32(np.mean(distortion, dtype=np.float32)),
-          avg_sparsity=F32(np.mean(sparsity, dtype=np.float32)),
-          step_size=step_size)
+      measurements = collections.OrderedDict(rnd.measurements)
+      measurements["step_size"] = step_size
       return tc.MeasuredProcessOutput(state=next_state,
-                                      result=_values.finish(out, shape, host),
+                                      result=_values.finish(rnd.result, shape, host),
                                       measurements=measurements)
 
     return tc.AggregationProcess(init_fn, next_fn)

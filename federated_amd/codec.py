@@ -165,24 +165,68 @@ def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None, presca
 
 def _repack(batch, sub, bad, caps):
   """A batch with capacities `caps` holding batch's clients, except clients `bad`
-  (in order), which come from `sub`."""
-  out = EncodedBatch(batch.P, batch.nclients, list(caps), batch.device)
-  T1 = batch.T + 1
-  T = batch.T
-  src_of = {int(c): (sub, i) for i, c in enumerate(bad)}
+  (ascending), which come from `sub`.
+
+  The per-client arrays move with one whole copy plus one ``index_copy_`` of the
+  re-encoded rows each; the code bytes with one copy per run of consecutive kept
+  clients (their relative layout is unchanged) and one per re-encoded client --
+  O(len(bad)) device copies, not O(C).
+  """
+  C, T = batch.nclients, batch.T
+  out = EncodedBatch(batch.P, C, list(caps), batch.device)
+  bad = np.asarray(bad, np.int64)
+  sel = torch.from_numpy(bad).to(batch.device)
+  for name, width in (("idx", T + 1), ("total_bits", 1), ("dist_part", T), ("nnz_part", T)):
+    dst, src, rep = getattr(out, name), getattr(batch, name), getattr(sub, name)
+    dst.copy_(src)
+    dst.view(C, width).index_copy_(0, sel, rep.view(len(bad), width))
   nbytes = batch.nbytes()
   sub_nbytes = sub.nbytes()
-  for c in range(batch.nclients):
-    b, i = src_of.get(c, (batch, c))
-    n = int(sub_nbytes[i] if b is sub else nbytes[c])
-    o_src, o_dst = int(b.offs_host[i]), int(out.offs_host[c])
-    out.stream[o_dst:o_dst + n].copy_(b.stream[o_src:o_src + n])
-    out.idx[c * T1:(c + 1) * T1].copy_(b.idx[i * T1:(i + 1) * T1])
-    out.total_bits[c:c + 1].copy_(b.total_bits[i:i + 1])
-    out.dist_part[c * T:(c + 1) * T].copy_(b.dist_part[i * T:(i + 1) * T])
-    out.nnz_part[c * T:(c + 1) * T].copy_(b.nnz_part[i * T:(i + 1) * T])
+  is_bad = np.zeros(C, bool)
+  is_bad[bad] = True
+  c = 0
+  while c < C:
+    if is_bad[c]:
+      c += 1
+      continue
+    e = c
+    while e + 1 < C and not is_bad[e + 1]:
+      e += 1
+    lo, n = int(batch.offs_host[c]), int(batch.offs_host[e] - batch.offs_host[c] + nbytes[e])
+    o = int(out.offs_host[c])
+    out.stream[o:o + n].copy_(batch.stream[lo:lo + n])
+    c = e + 1
+  for i, c in enumerate(bad):
+    n, o_src, o_dst = int(sub_nbytes[i]), int(sub.offs_host[i]), int(out.offs_host[c])
+    out.stream[o_dst:o_dst + n].copy_(sub.stream[o_src:o_src + n])
   out.overflow.zero_()
   return out
+
+
+class CapacityHint:
+  """Host-side per-process memory of the code sizes of the previous round.
+
+  A round's code size changes slowly between rounds (same step, similar deltas),
+  so the next round's stream capacities are sized from the largest client code
+  of the last one (+ 1/8 + 4 KiB slack) instead of ``default_capacity``'s 4
+  bits/element: dense rounds (e.g. 8-bit steps, ~10 bits/element) then encode
+  once instead of overflowing every client and encoding twice.  Overflow stays
+  handled (``quantize_encode_checked`` re-encodes only the clients that did).
+  """
+
+  def __init__(self):
+    self.max_bytes = None
+    self.P = None
+
+  def caps(self, P, nclients):
+    if self.max_bytes is None or self.P != int(P):
+      return [default_capacity(P)] * int(nclients)
+    cap = min(_round_up(self.max_bytes + self.max_bytes // 8 + 4096, _ALIGN), worst_case_capacity(P))
+    return [cap] * int(nclients)
+
+  def update(self, batch):
+    self.P = batch.P
+    self.max_bytes = int(batch.nbytes().max()) if batch.nclients else 0
 
 
 def rlgamma_encode(qs, caps=None):
@@ -348,10 +392,17 @@ def onebit_encode(xs, threshold=0.0):
   return masks, means, dist
 
 
-def onebit_decode_sum(masks, means, nclients, P):
-  out = torch.empty(int(P), dtype=torch.float32, device=masks.device)
-  _lib.call("fc_onebit_decode_sum", _lib.ptr(masks), _lib.ptr(means), int(nclients), int(P),
-            _lib.ptr(out), _lib.stream_handle())
+def onebit_decode_sum(masks, means, nclients, P, out=None, words=None, stream=None):
+  """Client-order float32 sum of the decoded one-bit values; words=(begin, end)
+  restricts it to mask words [begin, end) (elements 32 begin .. 32 end)."""
+  if out is None:
+    out = torch.empty(int(P), dtype=torch.float32, device=masks.device)
+  if words is None:
+    _lib.call("fc_onebit_decode_sum", _lib.ptr(masks), _lib.ptr(means), int(nclients), int(P),
+              _lib.ptr(out), _lib.stream_handle(stream))
+  else:
+    _lib.call("fc_onebit_decode_sum_range", _lib.ptr(masks), _lib.ptr(means), int(nclients), int(P),
+              int(words[0]), int(words[1]), _lib.ptr(out), _lib.stream_handle(stream))
   return out
 
 

@@ -2924,6 +2924,9 @@ __global__ __launch_bounds__(kThreads) void k_finalize(const float* dist_part, c
 #endif
 constexpr int kObThreads = FC_OB_THREADS;
 constexpr int kObWaves = kObThreads / 64;
+// distortion / sum x^2 below which the one-pass expansion is recomputed term by
+// term (float64 sums of x and x^2: relative error <= ~1e-11 of sum x^2)
+constexpr double kObCancel = 1.0 / (1 << 20);
 
 __device__ __forceinline__ uint32_t dpp_row_shl(uint32_t x, int n) {
   // lane l reads lane l + n of its 16-lane row (0 past the row end)
@@ -2985,8 +2988,8 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
   auto do_tile = [&](int64_t tile, const f4v (&raw)[8]) {
     const int64_t base = tile * 2048;
     const bool full = base + 2048 <= P;
-    float p1 = 0.0f, q1 = 0.0f;
-    double p2[2] = {0.0, 0.0}, q2[2] = {0.0, 0.0};  // two chains each
+    double p1[2] = {0.0, 0.0}, q1[2] = {0.0, 0.0};  // two chains each
+    double p2[2] = {0.0, 0.0}, q2[2] = {0.0, 0.0};
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int64_t e = base + 256 * k + 4 * lane;
@@ -3001,14 +3004,13 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
         nib |= ab ? (1u << i) : 0u;
         const double vd = (double)v;
         if (KIND == 0) {
-          p1 += v;
+          p1[k & 1] += vd;
           p2[k & 1] = fma(vd, vd, p2[k & 1]);
-          const float t = ab ? v : 0.0f;
-          q1 += t;
           const double td = ab ? vd : 0.0;
+          q1[k & 1] += td;
           q2[k & 1] = fma(td, td, q2[k & 1]);
         } else {
-          p1 += fabsf(v);
+          p1[k & 1] += fabs(vd);
           p2[k & 1] = fma(vd, vd, p2[k & 1]);
         }
       }
@@ -3019,10 +3021,10 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
       wd |= dpp_row_shl(wd, 4) << 16;
       if ((lane & 7) == 0) wordbuf[wv][8 * k + (lane >> 3)] = wd;
     }
-    s1 += (double)p1;
+    s1 += p1[0] + p1[1];
     s2 += p2[0] + p2[1];
     if (KIND == 0) {
-      a1 += (double)q1;
+      a1 += q1[0] + q1[1];
       a2 += q2[0] + q2[1];
     }
     __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses execute in order
@@ -3091,7 +3093,41 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
     }
     means[2 * c] = mb;
     means[2 * c + 1] = ma;
-    dist[c] = d_ > 0.0 ? d_ : 0.0;
+    // The expansion cancels when the spread is tiny next to the values (e.g. x =
+    // 1000 +- 1e-3): its float64 rounding (~1e-16 S2 per add) is then no longer
+    // small against the distortion.  Such a client is flagged (-1) and
+    // k_mask_distortion recomputes sum (x - decoded)^2 term by term, as TF does.
+    dist[c] = (d_ > kObCancel * S2) ? d_ : (S2 > 0.0 ? -1.0 : 0.0);
+  }
+}
+
+// Exact distortion of the clients k_mask_encode flagged (dist[c] < 0): one
+// workgroup per client, every term (x - decoded)^2 from the float32 difference
+// (one_bit_sgd.py:76-78 / drive.py:69-70), float64 sums in a fixed order.
+// Unflagged clients exit at once.
+template <int KIND>
+__global__ __launch_bounds__(kObThreads) void k_mask_distortion(const float* const* xs, int64_t P, float thr,
+                                                                const float* means, double* dist) {
+  __shared__ double red[kObWaves];
+  const int c = blockIdx.x;
+  if (!(dist[c] < 0.0)) return;
+  const float* __restrict__ x = xs[c];
+  const float mb = means[2 * c], ma = means[2 * c + 1];
+  double s = 0.0;
+  for (int64_t e = threadIdx.x; e < P; e += kObThreads) {
+    const float v = x[e] + 0.0f;
+    const float dec = KIND == 0 ? (!(v < thr) ? ma : mb) : (v < 0.0f ? mb : ma);
+    const double d = (double)(v - dec);
+    s = fma(d, d, s);
+  }
+  s = wave_sum_f64(s);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) red[wv] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kObWaves; ++w) t += red[w];
+    dist[c] = t;
   }
 }
 
@@ -3100,10 +3136,10 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
 // (TF's mask * ma + (1 - mask) * mb), summed in float32 as the reference's
 // accumulator.  The select is one bitop3 on the float bits.
 __global__ __launch_bounds__(256) void k_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t n,
-                                                           int64_t P, float* out) {
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                           int64_t P, int64_t w_begin, int64_t w_end, float* out) {
+  const int64_t w = w_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nw = (P + 31) / 32;
-  if (w >= nw) return;
+  if (w >= w_end) return;
   float s[32];
 #pragma unroll
   for (int k = 0; k < 32; ++k) s[k] = 0.0f;
@@ -3777,7 +3813,10 @@ int fc_drive_encode(const float* const* xs, int32_t nclients, int64_t P, int min
   if (!xs || !masks || !means || !dist) return fail(-1, "null pointer");
   hipLaunchKernelGGL(k_mask_encode<1>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, 0.0f,
                      min_distortion, masks, means, dist);
-  return check_launch("k_mask_encode<1>");
+  if (const int rc = check_launch("k_mask_encode<1>")) return rc;
+  hipLaunchKernelGGL(k_mask_distortion<1>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, 0.0f,
+                     (const float*)means, dist);
+  return check_launch("k_mask_distortion<1>");
 }
 
 int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, int64_t seed0, int64_t seed1,
@@ -3867,17 +3906,28 @@ int fc_onebit_encode(const float* const* xs, int32_t nclients, int64_t P, float 
   if (!xs || !masks || !means || !dist) return fail(-1, "null pointer");
   hipLaunchKernelGGL(k_mask_encode<0>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, threshold,
                      0, masks, means, dist);
-  return check_launch("k_mask_encode<0>");
+  if (const int rc = check_launch("k_mask_encode<0>")) return rc;
+  hipLaunchKernelGGL(k_mask_distortion<0>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P,
+                     threshold, (const float*)means, dist);
+  return check_launch("k_mask_distortion<0>");
+}
+
+int fc_onebit_decode_sum_range(const uint32_t* masks, const float* means, int32_t nclients, int64_t P,
+                               int64_t word_begin, int64_t word_end, float* out, void* stream) {
+  if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
+  if (!masks || !means || !out) return fail(-1, "null pointer");
+  const int64_t nw = (P + 31) / 32;
+  if (word_begin < 0 || word_end > nw || word_begin > word_end) return fail(-1, "bad word range");
+  if (word_begin == word_end) return 0;
+  const int64_t n = word_end - word_begin;
+  hipLaunchKernelGGL(k_onebit_decode_sum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     masks, means, nclients, P, word_begin, word_end, out);
+  return check_launch("k_onebit_decode_sum");
 }
 
 int fc_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t nclients, int64_t P, float* out,
                          void* stream) {
-  if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
-  if (!masks || !means || !out) return fail(-1, "null pointer");
-  const int64_t nw = (P + 31) / 32;
-  hipLaunchKernelGGL(k_onebit_decode_sum, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     masks, means, nclients, P, out);
-  return check_launch("k_onebit_decode_sum");
+  return fc_onebit_decode_sum_range(masks, means, nclients, P, 0, (P + 31) / 32, out, stream);
 }
 
 }  // extern "C"

@@ -11,10 +11,14 @@ compute for the HIP codec, called through ``tf.numpy_function``:
 
 * client ``quantize`` (quantize_encode.py:139-156) + ``tfc.run_length_gamma_encode``
   (elias_gamma_encode.py:98) -> one ``fc_quantize_encode`` launch for the client;
-  the client's message is the TFC byte string plus the encoder's decoder index
-  (8 bytes per 1024 elements, 0.06 bit/element; it travels beside the code the
-  way QSGD's norm travels beside its code, qsgd.py:79), and ``avg_bitrate`` counts
-  the code bytes only, as the reference;
+  the client step is ``normalize_fn(value) * step`` (quantize_encode.py:145; the
+  norm from ``fc_client_norms``);
+  WIRE CHANGE: the client's message is the pair ``(code, index)`` of two
+  ``tf.string``s instead of the reference's single ``tf.string`` code
+  (elias_gamma_encode.py:97-109): the TFC byte string, unchanged, plus the
+  encoder's decoder index (8 bytes per 1024 elements, 0.06 bit/element), which
+  travels beside the code the way QSGD's norm travels beside its code
+  (qsgd.py:79).  ``avg_bitrate`` counts the code bytes only, as the reference;
 * server ``federated_aggregate`` accumulate (elias_gamma_encode.py:69-73) ->
   ``fc_decode_accumulate`` of one client into the running int32 sum;
   merge (:75-77) is an int32 add;
@@ -39,15 +43,19 @@ def _tf():
   return tf, tff
 
 
-def _encode_one(x, step, seed, mode):
-  """numpy_function body: one client -> (code bytes, index bytes, distortion, sparsity, noise)."""
+def _encode_one(x, step, seed, mode, norm_kind=None):
+  """numpy_function body: one client -> (code bytes, index bytes, distortion, sparsity, noise).
+
+  ``norm_kind``: the factory's normalisation (quantize_encode.py:145: the client
+  step is ``normalize_fn(value) * step``), None for "constant"."""
   import torch  # pylint: disable=g-import-not-at-top
   from federated_amd import _lib  # pylint: disable=g-import-not-at-top
   from federated_amd import codec  # pylint: disable=g-import-not-at-top
   x = torch.from_numpy(np.ascontiguousarray(x, np.float32).reshape(-1)).cuda()
   P = x.numel()
   seeds = torch.as_tensor(np.asarray(seed, np.int64).reshape(1, 2))
-  batch = codec.quantize_encode_checked([x], float(step), seeds, int(mode))
+  norms = codec.client_norms([x], norm_kind) if norm_kind else None
+  batch = codec.quantize_encode_checked([x], float(step), seeds, int(mode), norms=norms)
   dist, nnz = codec.finalize(batch)
   code = batch.client_code(0)
   index = batch.idx.cpu().numpy().tobytes()
@@ -84,12 +92,13 @@ def quantize_encode_process(value_type, factory):
   shape = value_type.shape
   P = int(np.prod(shape)) if len(shape) else 1
   mode = factory._mode  # pylint: disable=protected-access
+  norm_kind = factory._norm_kind  # pylint: disable=protected-access
 
   @tff.tf_computation(value_type, tf.float32)
   def quantize(value, step_size):
     seed = tf.cast(tf.stack([tf.timestamp() * 1e6, tf.timestamp() * 1e6]), dtype=tf.int64)
     code, index, distortion, sparsity, noise = tf.numpy_function(
-        lambda x, s, sd: _encode_one(x, s, sd, mode), [value, step_size, seed],
+        lambda x, s, sd: _encode_one(x, s, sd, mode, norm_kind), [value, step_size, seed],
         [tf.string, tf.string, tf.float32, tf.float32, tf.float32])
     return (code, index), tf.reshape(noise, shape), distortion, sparsity
 

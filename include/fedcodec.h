@@ -199,6 +199,12 @@ int fc_onebit_encode(const float* const* xs, int32_t nclients, int64_t P, float 
                      uint32_t* masks, float* means, double* dist, void* stream);
 int fc_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t nclients,
                          int64_t P, float* out, void* stream);
+/* The same over mask words [word_begin, word_end) only (elements 32 word_begin ..
+ * min(P, 32 word_end)): the multi-GPU round sums one element range while the
+ * previous range's float32 all-reduce runs (one_bit_sgd.py:87-112 per range). */
+int fc_onebit_decode_sum_range(const uint32_t* masks, const float* means, int32_t nclients,
+                               int64_t P, int64_t word_begin, int64_t word_end, float* out,
+                               void* stream);
 
 /* DRIVE: masks bit set = x >= 0 (not negative), means[2c] = -scale, means[2c+1] =
  * +scale with scale = ||x||_2^2 / ||x||_1 (min_distortion = 0, divide_no_nan) or

@@ -102,11 +102,14 @@ def one_bit_sgd_next(client_values, threshold=0.0):
   acc = np.zeros(P, np.float32)
   dists = []
   for x in xs:
-    above = (x >= F32(threshold)).astype(np.float32)                        # :63-67
+    above = (x >= F32(threshold)).astype(np.float32)                        # :58-61
     below = F32(1.0) - above
-    mb = F32(np.sum(x * below, dtype=np.float64) / max(np.sum(below), 1.0))  # :69-74
-    ma = F32(np.sum(x * above, dtype=np.float64) / max(np.sum(above), 1.0))
+    # :63-68: float32 reduce_sum (restated as the correctly rounded float32 of the
+    # float64 sum) divided in float32 by the float32 count
+    mb = F32(F32(np.sum(x * below, dtype=np.float64)) / F32(max(np.sum(below), 1.0)))
+    ma = F32(F32(np.sum(x * above, dtype=np.float64)) / F32(max(np.sum(above), 1.0)))
     dec = (above * ma + (F32(1.0) - above) * mb).astype(np.float32)         # :45-54
+    # :76-78
     dists.append(F32(np.sum((x - dec).astype(np.float64) ** 2) / P))
     acc = (acc + dec).astype(np.float32)                                     # :97-100
   return acc, collections.OrderedDict(avg_bitrate=F32((F32(P) + F32(64.0)) / F32(P)),

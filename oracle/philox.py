@@ -78,6 +78,19 @@ def random_bits(n, seed):
   return out[:n]
 
 
+def random_bits_at(idx, seed):
+  """``random_bits(n, seed)[idx]`` for element indices ``idx`` only (the same
+  counter arithmetic: element i is lane i % 4 of counter + i // 4), so sampled
+  positions of a large tensor can be checked without drawing the whole stream."""
+  key, counter = seed_to_key_counter(seed)
+  idx = np.asarray(idx, np.int64)
+  g = (idx // 4).astype(np.uint64)
+  c0 = (g & np.uint64(_M32)).astype(np.uint32)
+  c1 = (g >> np.uint64(32)).astype(np.uint32)
+  r = np.stack(philox4x32_10([c0, c1, np.uint32(counter[2]), np.uint32(counter[3])], key), axis=1)
+  return r[np.arange(idx.size), idx % 4]
+
+
 def stateless_uniform(n, seed, minval=0.0, maxval=1.0):
   """``tf.random.stateless_uniform([n], seed, minval, maxval, float32)``.
 

@@ -79,6 +79,17 @@ def stochastic_quantize(value, step_size, seed):
   return f32_to_i32(rounded)
 
 
+def stochastic_quantize_at(values, idx, step_size, seed):
+  """``stochastic_quantize(x, step_size, seed)[idx]`` from ``values = x[idx]``
+  (elementwise: element i needs only x[i] and stream element i)."""
+  scaled = _div(np.asarray(values, np.float32), step_size)
+  fl = np.floor(scaled)
+  with np.errstate(invalid="ignore"):
+    prob = ftz(scaled - fl)
+  rnd = philox.uint32_to_float(philox.random_bits_at(idx, seed))
+  return f32_to_i32(np.where(rnd <= prob, np.ceil(scaled), fl))
+
+
 # quantize_utils.py:57-59
 def generate_noise(seed, n):
   return philox.stateless_uniform(n, seed, -0.5, 0.5)

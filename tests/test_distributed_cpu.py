@@ -120,3 +120,68 @@ def test_two_rank_slab_allreduce_matches_single_process():
   want = ((want + 2**31) % 2**32 - 2**31).astype(np.int32)
   for r in range(world):
     np.testing.assert_array_equal(out[r], want)
+
+
+def _means_worker(rank, world, port, out):
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  # rank r holds r + 1 clients with values r + 1 (sums [n, 2n]); rank 2 none
+  n = rank + 1 if rank < 2 else 0
+  means, total = distributed.global_means([float(n * (rank + 1)), 2.0 * n * (rank + 1)], n,
+                                          torch.device("cpu"))
+  out[rank] = (means.tolist(), total)
+  dist.destroy_process_group()
+
+
+def test_global_means_three_ranks_one_empty():
+  """elias_gamma_encode.py:100-108 / quantize_encode.py:184-185: federated_mean over
+  every client of every rank, ranks may hold no clients."""
+  mgr = mp.Manager()
+  out = mgr.dict()
+  mp.spawn(_means_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+  # clients: [1] from rank 0, [2, 2] from rank 1 -> mean 5/3, second sum twice that
+  for r in range(3):
+    means, total = out[r]
+    assert total == 3
+    np.testing.assert_allclose(means, [5.0 / 3.0, 10.0 / 3.0], rtol=1e-15)
+
+
+def _onebit_worker(rank, world, port, C, P, out):
+  """The one-bit round's reduction (distributed.onebit_round): each rank's
+  client-order float32 sum of its decoded clients (oracle decode standing in for
+  fc_onebit_decode_sum), then a float32 SUM all-reduce and the global distortion
+  mean via global_means."""
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  from oracle import aggregators as oagg  # pylint: disable=g-import-not-at-top
+  rng = np.random.default_rng(11)
+  xs = [(rng.standard_normal(P) * 2 + 0.3).astype(np.float32) for _ in range(C)]
+  lo, hi = distributed.client_shard(C, world, rank)
+  part, meas = oagg.one_bit_sgd_next(xs[lo:hi], 0.0)
+  t = torch.from_numpy(part.copy())
+  distributed.allreduce_sum_(t)
+  (m,), total = distributed.global_means([float(meas["avg_distortion"]) * (hi - lo)], hi - lo,
+                                         torch.device("cpu"))
+  out[rank] = (t.numpy().copy(), m, total)
+  dist.destroy_process_group()
+
+
+def test_two_rank_onebit_reduction_matches_single_process():
+  """Config 5's 8-GPU split, reduction side (one_bit_sgd.py:87-112): float32 partial
+  sums all-reduced equal the single-process client-order sum within the
+  float-association tolerance rel 1e-6 * C."""
+  from oracle import aggregators as oagg  # pylint: disable=g-import-not-at-top
+  C, P, world = 7, 5003, 2
+  mgr = mp.Manager()
+  out = mgr.dict()
+  mp.spawn(_onebit_worker, args=(world, _free_port(), C, P, out), nprocs=world, join=True)
+  rng = np.random.default_rng(11)
+  xs = [(rng.standard_normal(P) * 2 + 0.3).astype(np.float32) for _ in range(C)]
+  want, meas = oagg.one_bit_sgd_next(xs, 0.0)
+  for r in range(world):
+    got, m, total = out[r]
+    assert total == C
+    np.testing.assert_allclose(got, want, rtol=1e-6 * C, atol=1e-6 * C * float(np.max(np.abs(want))))
+    np.testing.assert_allclose(m, meas["avg_distortion"], rtol=1e-6)

@@ -10,6 +10,7 @@ BASELINE.json ``configs`` (SURVEY.md §8 config sizes):
      and 257 clients x 25 M (more clients than decoder lanes per tile, an odd
      client count for the encoder's multiply-high ticket division);
   5. one-bit SGD codec at P = 25,000,000 (one_bit_sgd.py:45-112).
+  4. one GPU's share of config 4: 64 clients x 11,000,000 (ResNet-18), stochastic;
 Configs 4 and 5's 8-GPU splits are covered by the distributed tests.
 
 Checks, by what the oracle (CPU restatement) can afford in seconds:
@@ -130,8 +131,63 @@ def test_headline_shape_round(gpu, C, mode):
   want = _hip_quantize_sum(rows, step, seeds, mode)
   assert torch.equal(s, want)
   np.testing.assert_array_equal(out.cpu().numpy(), oq.uniform_dequantize(want.cpu().numpy(), F32(step)))
+  _check_sum_sampled(rows, s, step, seeds, mode)
   # whole-batch code length: the sum of every client's bit count is what the decoder consumed
   assert int(batch.bits().min()) > 0
+  del rows, batch, s, out, want
+  _release()
+
+
+def _check_sum_sampled(rows, s, step, seeds, mode, n=20_000, seed=8):
+  """The full round's int32 sum against the ORACLE at n sampled positions, every
+  client's term restated there (oracle.quantize_utils.stochastic_quantize_at: the
+  quantiser is elementwise and stream element i needs only its counter)."""
+  P = rows[0].numel()
+  idx = np.sort(np.random.default_rng(seed).choice(P, n, replace=False))
+  it = torch.from_numpy(idx).to(rows[0].device)
+  vals = torch.stack([r[it] for r in rows]).cpu().numpy()
+
+  def one(c):
+    if mode == "uniform":
+      return oq.uniform_quantize(vals[c], F32(step)).astype(np.int64)
+    return oq.stochastic_quantize_at(vals[c], idx, F32(step), tuple(seeds[c])).astype(np.int64)
+  acc = np.zeros(n, np.int64)
+  with ThreadPoolExecutor(WORKERS) as ex:
+    for q in ex.map(one, range(len(rows))):
+      acc += q
+  np.testing.assert_array_equal(s[it].cpu().numpy(), oagg.wrap_i32(acc))
+
+
+def test_config4_share_round(gpu):
+  """One GPU's share of config 4 (CIFAR-100 ResNet-18 deltas, 512 clients x 11 M
+  over 8 GPUs): 64 clients x 11,000,000, stochastic step 0.5 (sigma 1), through
+  QuantizeEncodeFactory at its default settings.  Codes of three clients
+  byte-identical to the oracle; the int32 sum against the oracle at sampled
+  positions of every client and against the HIP elementwise quantiser in full;
+  the result bit-exact; a second round reuses the first round's code sizes
+  (no overflow re-encode)."""
+  from federated_amd.aggregators import quantize_encode  # pylint: disable=g-import-not-at-top
+  C, P, step = 64, 11_000_000, 0.5
+  g = torch.Generator(device=gpu)
+  rows = []
+  for c in range(C):
+    g.manual_seed(11000 + c)
+    rows.append(torch.randn(P, generator=g, device=gpu, dtype=torch.float32))
+  seeds = np.array([[300 + c, 7 * c + 2] for c in range(C)], np.int64)
+  batch, s, out = _round(rows, step, seeds, "stochastic")
+  picks = (0, 33, 63)
+  _check_codes(batch, {c: rows[c].cpu().numpy() for c in picks}, picks, step, seeds, "stochastic")
+  want = _hip_quantize_sum(rows, step, seeds, "stochastic")
+  assert torch.equal(s, want)
+  _check_sum_sampled(rows, s, step, seeds, "stochastic")
+  res_want = oq.uniform_dequantize(want.cpu().numpy(), F32(step))
+  np.testing.assert_array_equal(out.cpu().numpy(), res_want)
+  process = quantize_encode.QuantizeEncodeFactory(step, rounding_type="stochastic").create((np.float32, (P,)))
+  state = process.initialize()
+  for _ in range(2):
+    r = process.next(state, rows, seeds=seeds)
+    np.testing.assert_array_equal(r.result.cpu().numpy(), res_want)
+    state = r.state
   del rows, batch, s, out, want
   _release()
 
