@@ -82,6 +82,46 @@ class Workspace:
 _WS = Workspace()
 
 
+class SegWorkspace:
+  """Grow-only device workspace of the segmented encoder (256-byte aligned)."""
+
+  def __init__(self):
+    self.buf = None
+
+  def get(self, nclients, P, nseg, max_cap, device):
+    need = int(_lib.load().fc_segmented_workspace_bytes(int(nclients), int(P), int(nseg), int(max_cap)))
+    if need < 0:
+      return None
+    if self.buf is None or self.buf.numel() < need + 256 or self.buf.device != device:
+      self.buf = None
+      self.buf = torch.empty(_round_up(need + 256, 256), dtype=torch.uint8, device=device)
+    off = (-self.buf.data_ptr()) % 256
+    return self.buf[off:off + need]
+
+
+_SEG_WS = SegWorkspace()
+
+
+def auto_segments(nclients, P):
+  """Segments per client for the segmented encoder (1: none).
+
+  The super-tile encoder wants about a thousand rows in flight; a batch of at
+  most 256 clients of >= 2^21 elements is cut into 1024 / C segments per
+  client (each >= 2^18 elements).  ``FEDCODEC_SEGMENTS`` overrides (1 = off).
+  """
+  import os  # pylint: disable=g-import-not-at-top
+  env = os.environ.get("FEDCODEC_SEGMENTS")
+  if env:
+    return max(1, int(env))
+  C, P = int(nclients), int(P)
+  if C > 256 or P < (1 << 21):
+    return 1
+  k = 1024 // C
+  while k > 1 and P // k < (1 << 18):
+    k //= 2
+  return max(1, min(63, k))
+
+
 def _ptr_array(tensors, device):
   return torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64, device=device)
 
@@ -102,12 +142,14 @@ def _rows(xs, dtype):
 
 
 def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, ptrs=None,
-                    out=None, P=None, prescale=None):
+                    out=None, P=None, prescale=None, segments=None):
   """fc_quantize_encode over a batch.  ``xs``: [C, P] tensor or list of tensors.
 
   ``seeds``: int64 tensor [C, 2] (device or host).  ``norms``: optional device
   float32 [C] (client step = norms[c] * step).  Returns an EncodedBatch.
   ``ptrs``/``P``/``out`` let hot loops reuse a pointer array and buffers.
+  ``segments``: segments per client for fc_quantize_encode_segmented (same
+  output bit for bit; None: ``auto_segments``, 1: off).
   """
   _lib.require_gpu()
   if ptrs is None:
@@ -121,6 +163,17 @@ def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, p
   seeds = torch.as_tensor(seeds, dtype=torch.int64).reshape(C, 2).to(device)
   if out is None:
     out = EncodedBatch(P, C, caps if caps is not None else [default_capacity(P)] * C, device)
+  nseg = auto_segments(C, P) if segments is None else int(segments)
+  if nseg > 1:
+    max_cap = int(out.caps_host.max())
+    sws = _SEG_WS.get(C, P, nseg, max_cap, device)
+    if sws is not None:
+      _lib.call("fc_quantize_encode_segmented", _lib.ptr(ptrs), C, P, float(step), _lib.ptr(norms),
+                _lib.ptr(prescale), _lib.ptr(seeds), int(mode), nseg, max_cap, _lib.ptr(out.stream),
+                _lib.ptr(out.stream_off), _lib.ptr(out.stream_cap), _lib.ptr(out.idx), _lib.ptr(out.total_bits),
+                _lib.ptr(out.dist_part), _lib.ptr(out.nnz_part), _lib.ptr(out.overflow), _lib.ptr(sws),
+                sws.numel(), _lib.stream_handle(stream))
+      return out
   ws = _WS.get(C, P, device)
   _lib.call("fc_quantize_encode", _lib.ptr(ptrs), C, P, float(step), _lib.ptr(norms),
             _lib.ptr(prescale), _lib.ptr(seeds), int(mode), _lib.ptr(out.stream), _lib.ptr(out.stream_off),
@@ -135,7 +188,7 @@ def check_overflow(batch):
   return np.nonzero(batch.overflow.cpu().numpy())[0]
 
 
-def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None, prescale=None):
+def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None, prescale=None, segments=None):
   """quantize_encode; clients whose code overflowed their capacity are re-encoded.
 
   The encoder reports every client's exact bit length even on overflow, so only
@@ -144,7 +197,7 @@ def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None, presca
   recomputed).  A client's code does not depend on the rest of its batch.
   """
   rows = _rows(xs, torch.float32)
-  batch = quantize_encode(rows, step, seeds, mode, norms=norms, caps=caps, prescale=prescale)
+  batch = quantize_encode(rows, step, seeds, mode, norms=norms, caps=caps, prescale=prescale, segments=segments)
   bad = check_overflow(batch)
   if not len(bad):
     return batch
@@ -153,7 +206,7 @@ def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None, presca
   sel = torch.as_tensor(bad, dtype=torch.int64, device=device)
   seeds = torch.as_tensor(seeds, dtype=torch.int64).reshape(C, 2).to(device)
   need = (batch.bits()[bad] + 7) // 8 + 256
-  sub = quantize_encode([rows[c] for c in bad], step, seeds[sel], mode,
+  sub = quantize_encode([rows[c] for c in bad], step, seeds[sel], mode, segments=1,
                         norms=None if norms is None else norms[sel], caps=list(need),
                         prescale=None if prescale is None else
                         torch.as_tensor(prescale).reshape(C, 2).to(device)[sel].contiguous())

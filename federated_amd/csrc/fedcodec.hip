@@ -279,6 +279,8 @@ struct EncodeArgs {
   uint32_t div_m, div_l;  // ticket / nclients by multiply-high (Granlund-Montgomery)
   int32_t lb_lane0;       // first lane whose status the look-back prefetches (64 - window)
   int32_t T2;             // super-tiles (two tiles) per client: k_encode2's tickets and statuses
+  const int64_t* elem_off;  // nullable [C]: element offset (multiple of 4) of row c in its client's
+                            // tensor -- the row is a segment; its Philox stream continues there
 };
 
 // The launch's EncodeArgs re-read from the kernarg segment (k_encode and
@@ -746,6 +748,7 @@ struct ClientQ {
   float s0, s1;  // pre-scales (TFF clipping factor, MeanFactory weight)
   bool pre;
   Key4 key;
+  uint32_t gofs;  // Philox group of the row's element 0 (a segment of a longer client)
 };
 
 // Quantise one chunk of 4 consecutive elements starting at e0.
@@ -758,7 +761,7 @@ __device__ __forceinline__ void quant_chunk(const ClientQ& cq, int64_t e0, int64
     for (int k = 0; k < 4; ++k) q4[k] = (int32_t)r4[k];
   } else {
     uint4 rb = make_uint4(0, 0, 0, 0);
-    if (MODE != FC_UNIFORM) rb = philox_group(cq.key, (uint32_t)(e0 >> 2));
+    if (MODE != FC_UNIFORM) rb = philox_group(cq.key, (uint32_t)(e0 >> 2) + cq.gofs);
     const uint32_t rr[4] = {rb.x, rb.y, rb.z, rb.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1068,7 +1071,7 @@ struct alignas(64) ClientParam {
   const uint32_t* x;         // the client's float32 (or int32) values
   uint32_t* out;             // stream_buf + stream_off[c]
   int64_t cap;               // stream_cap[c] (bytes)
-  int64_t pad;
+  int64_t gofs;              // Philox group of x[0]: elem_off[c] / 4 (segments), else 0
 };
 
 __global__ void k_client_params(EncodeArgs a, ClientParam* cp, int need_key) {
@@ -1088,7 +1091,7 @@ __global__ void k_client_params(EncodeArgs a, ClientParam* cp, int need_key) {
   p.x = (const uint32_t*)a.xs[c];
   p.out = (uint32_t*)(a.stream_buf + a.stream_off[c]);
   p.cap = a.stream_cap[c];
-  p.pad = 0;
+  p.gofs = a.elem_off ? a.elem_off[c] >> 2 : 0;
   cp[c] = p;
 }
 
@@ -1108,7 +1111,7 @@ __device__ __forceinline__ ClientParam ld_param(ConstParamPtr p) {
   r.x = p->x;
   r.out = p->out;
   r.cap = p->cap;
-  r.pad = 0;
+  r.gofs = p->gofs;
   return r;
 }
 
@@ -1120,6 +1123,7 @@ __device__ __forceinline__ ClientQ client_q_of(const ClientParam& p, bool pre) {
   r.s1 = p.s1;
   r.pre = pre;
   r.key = Key4{p.k0, p.k1, p.c2, p.c3};
+  r.gofs = (uint32_t)p.gofs;
   return r;
 }
 
@@ -1497,7 +1501,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
             for (int k = 0; k < 4; ++k) nnz += q4[k] != 0;
             cc = chunk_local(q4, rel0);
           } else {
-            const uint32_t g = (uint32_t)((tile_base + rel0) >> 2);
+            const uint32_t g = (uint32_t)((tile_base + rel0) >> 2) + cq.gofs;
             if (MODE == FC_DITHERED && !full)
               cc = quant_code_fast<MODE, DIV, PRE, true>(cq, g, raw[j], rel0, dist, nnz, clut,
                                                     (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - rel0)));
@@ -1871,7 +1875,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       uint64_t cacc[kChunks];
       uint32_t clen[kChunks];
       const int32_t hrel = h * kTE + lrel;
-      const uint32_t gbase = (uint32_t)(tile_base >> 2) + 4u * (uint32_t)lane;  // Philox counter of chunk 0
+      const uint32_t gbase = (uint32_t)(tile_base >> 2) + 4u * (uint32_t)lane + cq.gofs;  // Philox counter of chunk 0
 #pragma unroll
       for (int j = 0; j < kChunks; ++j) {
         const int32_t rel0 = hrel + 4 * j;
@@ -2255,6 +2259,9 @@ __device__ __noinline__ CodeVal slow_code(const uint8_t* base, int64_t cap, uint
 // 16-byte reads.  Loads are issued only at batch points the wave reaches
 // together every kDecBatch iterations, so the wave's in-order memory counter
 // does not make a lane wait for loads other lanes issued an iteration ago.
+#ifndef FC_DEC_SEL_REFILL
+#define FC_DEC_SEL_REFILL 0  // window refill by selects instead of a branch (A/B knob)
+#endif
 #ifndef FC_DEC_ABL
 #define FC_DEC_ABL 0  // decoder ablation bits (diagnostics only): 1 sums one bank per lane, 2 no sums, 8 eight clients' streams for all lanes
 #endif
@@ -2592,11 +2599,24 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       acc_add_at<PLANE>(relb, v, ptile, hib);
       cons += (int32_t)L;
     }
+#if FC_DEC_SEL_REFILL
+    {  // branch-free refill: selects instead of an exec-masked block
+      const bool need = fill - cons <= 32;
+      const uint32_t w = need ? (uint32_t)(r.rh >> 32) : 0u;
+      r.win |= (uint64_t)w << ((uint32_t)(32 - (fill - cons)) & 63u);
+      r.rh = need ? ((r.rh << 32) | (r.rl >> 32)) : r.rh;
+      r.rl = need ? (r.rl << 32) : r.rl;
+      r.rb -= need ? 32 : 0;
+      fill += need ? 32 : 0;
+      if (r.rb == 0) r.take_block();
+    }
+#else
     if (fill - cons <= 32) {  // (the blocks are zero past the segment end)
       const uint32_t w = r.pop32();
       r.win |= (uint64_t)w << (32 - (fill - cons));
       fill += 32;
     }
+#endif
     }
     if (stop) break;
   }
@@ -3466,7 +3486,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
                   const float* prescale, const int64_t* seeds, int mode, bool int_in, uint8_t* stream_buf,
                   const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
                   int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow,
-                  void* workspace, int64_t workspace_bytes, void* stream) {
+                  void* workspace, int64_t workspace_bytes, void* stream, const int64_t* elem_off = nullptr) {
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
   if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
   if (!xs || !stream_buf || !stream_off || !stream_cap || !idx || !total_bits || !overflow)
@@ -3483,6 +3503,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   if (hipMemsetAsync(workspace, 0, enc_zeroed_bytes(nclients, P), s) != hipSuccess) return fail(-10, "memset status");
   if (hipMemsetAsync(overflow, 0, sizeof(int32_t) * nclients, s) != hipSuccess) return fail(-10, "memset overflow");
   EncodeArgs a;
+  a.elem_off = elem_off;
   a.xs = xs;
   a.nclients = nclients;
   a.P = P;
@@ -3591,6 +3612,474 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   return check_launch("k_encode_exact");
 }
 
+// ---------------------------------------------------------------------------
+// Segmented encode (few clients per GPU).  The super-tile encoder needs about a
+// thousand clients in flight to keep its look-back off the critical path; with
+// fewer (the 8-GPU share of the headline: 128 clients) each client is cut into K
+// element segments (seg_elems, a multiple of 2048, plus a remainder) that are
+// encoded as independent "virtual clients" -- each continuing its client's
+// Philox stream at its element offset -- and then stitched into the client's
+// canonical stream:
+//   * a segment's first code carries the run from virtual position -1; it is
+//     replaced by the run from the client's last nonzero before the segment;
+//   * every segment's trailing zero-run code is dropped; the client's own
+//     trailing code (from its last nonzero) is appended at the end;
+//   * the bits in between move to their final offset (a funnel-shift copy),
+//     the decoder index entries are rebased, the distortion / nonzero partials
+//     copied to the client's tile slots.
+// The result is bit-identical to encoding the client in one piece.
+// ---------------------------------------------------------------------------
+struct SegPlan {       // one per segment, plus the client's trailing code (entry nseg)
+  int64_t O;           // output bit where the segment's (new) first code starts
+  int64_t len;         // output bits: new first run code + body (tail entry: tlen)
+  const uint8_t* src;  // the segment's virtual stream (nullptr for the tail entry)
+  int64_t gprev;       // the client's last nonzero before the segment (-1: none); tail: last overall
+  uint32_t newR;       // bits of the new first run code (tail entry: trailing code bits)
+  uint32_t dnew;       // its value (tail entry: the trailing code's value)
+  uint32_t srcbit;     // source bit where the body starts (after the old first run code)
+  uint32_t pad;
+};
+
+struct SegArgs {
+  const void* const* xs;
+  int32_t nclients, K, nseg;  // nseg = K (+1 with a remainder segment)
+  int64_t P, seg_elems, rem_elems;
+  int32_t Tv, Tr;             // tiles per main / remainder segment
+  const float* norms;
+  const float* prescale;
+  const int64_t* seeds;
+  // virtual clients: main v = c * K + k (k < K), remainder v = C * K + c
+  const float** vptr;
+  int64_t* voff;
+  int64_t* vseeds;
+  float* vnorms;
+  float* vpre;
+  int64_t* vstream_off;
+  int64_t* vstream_cap;
+  uint8_t* vstream;
+  int64_t vcap_main, vcap_rem;
+  uint64_t* vidx_main;        // [C * K][Tv + 1]
+  uint64_t* vidx_rem;         // [C][Tr + 1]
+  int64_t* vbits;             // [C * K + C]
+  float* vdist_main;          // [C * K][Tv]
+  float* vdist_rem;           // [C][Tr]
+  int32_t* vnnz_main;
+  int32_t* vnnz_rem;
+  int32_t* vovf;              // [C * K + C]
+  SegPlan* plan;              // [C][nseg + 1]
+  // the client batch
+  uint8_t* stream_buf;
+  const int64_t* stream_off;
+  const int64_t* stream_cap;
+  uint64_t* idx;
+  int64_t* total_bits;
+  float* dist_part;
+  int32_t* nnz_part;
+  int32_t* overflow;
+};
+
+__global__ void k_seg_setup(SegArgs a) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nv = (int64_t)a.nclients * a.K + (a.rem_elems > 0 ? a.nclients : 0);
+  if (v >= nv) return;
+  const int64_t nmain = (int64_t)a.nclients * a.K;
+  const bool main = v < nmain;
+  const int32_t c = (int32_t)(main ? v / a.K : v - nmain);
+  const int32_t k = (int32_t)(main ? v - (int64_t)c * a.K : a.K);
+  const int64_t off = (int64_t)k * a.seg_elems;
+  a.vptr[v] = (const float*)a.xs[c] + off;
+  a.voff[v] = off;
+  if (a.seeds) {
+    a.vseeds[2 * v] = a.seeds[2 * c];
+    a.vseeds[2 * v + 1] = a.seeds[2 * c + 1];
+  }
+  if (a.norms) a.vnorms[v] = a.norms[c];
+  if (a.prescale) {
+    a.vpre[2 * v] = a.prescale[2 * c];
+    a.vpre[2 * v + 1] = a.prescale[2 * c + 1];
+  }
+  a.vstream_off[v] = main ? v * a.vcap_main : nmain * a.vcap_main + (int64_t)c * a.vcap_rem;
+  a.vstream_cap[v] = main ? a.vcap_main : a.vcap_rem;
+  if (main && k == 0) {  // a client's first segment codes in place: its bits do not move
+    a.vstream_off[v] = (int64_t)((a.stream_buf + a.stream_off[c]) - a.vstream);
+    a.vstream_cap[v] = a.stream_cap[c];
+  }
+}
+
+__device__ __forceinline__ uint32_t glen64(uint64_t d) { return 2u * (63u - (uint32_t)__clzll(d)) + 1u; }
+
+// One wave per client, lane k = segment k: each segment's first / last nonzero
+// and old first / trailing codes, then the client's new first run codes (from the
+// exclusive max-scan of the segments' last nonzeros), output offsets and the
+// trailing code.
+__global__ __launch_bounds__(64) void k_seg_plan(SegArgs a) {
+  __shared__ int64_t lens[64];
+  __shared__ int64_t gls[64];
+  const int c = blockIdx.x;
+  const int k = threadIdx.x;
+  const bool live = k < a.nseg;
+  const bool main = k < a.K;
+  const int64_t v = main ? (int64_t)c * a.K + k : (int64_t)a.nclients * a.K + c;
+  const int64_t Pk = main ? a.seg_elems : a.rem_elems;
+  const int32_t Tk = main ? a.Tv : a.Tr;
+  const int64_t sk = (int64_t)k * a.seg_elems;
+  int64_t last = -1, len = 0, body = 0, gl = -1, f = -1;
+  uint32_t oldR = 0, ovf = 0;
+  const uint8_t* src = nullptr;
+  if (live) {
+    const uint64_t* vi = main ? a.vidx_main + v * (a.Tv + 1) : a.vidx_rem + (int64_t)c * (a.Tr + 1);
+    last = (int64_t)(vi[Tk] >> 36) - 1;
+    const int64_t nb = a.vbits[v];
+    src = a.vstream + a.vstream_off[v];
+    ovf = a.vovf[v] != 0;
+    if (last >= 0) {
+      // the segment's first code is gamma(f + 1): z zeros, then z + 1 value bits
+      // (its first words are stored even when the segment overflowed its staging)
+      const uint32_t* s32 = (const uint32_t*)src;
+      const uint64_t top = ((uint64_t)bswap32(s32[0]) << 32) | bswap32(s32[1]);
+      const uint32_t z = (uint32_t)__clzll(top);
+      const uint64_t d0 = (top << z) >> (63 - z);
+      f = (int64_t)d0 - 1;
+      oldR = 2 * z + 1;
+      const int64_t trail = last < Pk - 1 ? (int64_t)glen64((uint64_t)(Pk - last)) : 0;
+      body = nb - oldR - trail;
+      gl = sk + last;
+    }
+  }
+  gls[k] = gl;
+  __syncthreads();
+  int64_t gprev = -1;
+  for (int j = 0; j < k && j < a.nseg; ++j) gprev = max(gprev, gls[j]);
+  uint32_t newR = 0, dnew = 0;
+  if (live && last >= 0) {
+    dnew = (uint32_t)(sk + f - gprev);
+    newR = glen64(dnew);
+    len = newR + body;
+  }
+  lens[k] = live ? len : 0;
+  const uint64_t bad = __ballot(live && ovf != 0);
+  __syncthreads();
+  SegPlan* pl = a.plan + (int64_t)c * (a.nseg + 1);
+  int64_t O = 0;
+  for (int j = 0; j < k; ++j) O += lens[j];
+  if (live) {
+    SegPlan e;
+    e.O = O;
+    e.len = len;
+    e.src = src;
+    e.gprev = gprev;
+    e.newR = newR;
+    e.dnew = dnew;
+    e.srcbit = oldR;
+    e.pad = 0;
+    pl[k] = e;
+  }
+  if (k == 0) {
+    int64_t sum = 0, L = -1;
+    for (int j = 0; j < a.nseg; ++j) {
+      sum += lens[j];
+      L = max(L, gls[j]);
+    }
+    SegPlan t;
+    t.O = sum;
+    t.src = nullptr;
+    t.gprev = L;
+    t.srcbit = 0;
+    t.pad = 0;
+    t.newR = 0;
+    t.dnew = 0;
+    if (L < a.P - 1) {
+      t.dnew = (uint32_t)(a.P - L);
+      t.newR = glen64((uint64_t)(a.P - L));
+    }
+    t.len = t.newR;
+    pl[a.nseg] = t;
+    const int64_t total = sum + t.newR;
+    a.total_bits[c] = total;
+    a.overflow[c] = (bad != 0 || (total + 31) / 32 * 4 > a.stream_cap[c]) ? 1 : 0;
+  }
+}
+
+// bits [rel, rel + n) of an MSB-first code of `len` bits, right-aligned
+__device__ __forceinline__ uint32_t code_bits(uint32_t code, uint32_t len, uint32_t rel, uint32_t n) {
+  return (uint32_t)(((uint64_t)code >> (len - rel - n)) & ((1ull << n) - 1));
+}
+
+// The stitched words.  Persistent workgroups walk (client, block of 1024 words)
+// items; a thread takes 4 consecutive words: inside one segment's moved body (the
+// common case) they are a funnel shift of 5 source words and one 16-byte store;
+// otherwise each word is gathered from the (usually one or two) pieces it spans.
+// Bits past the client's last bit are zero, as the encoder's owner-written last word.
+constexpr int kSegGroups = 4;                      // 16-byte groups per thread per item
+constexpr int kSegWordsPerBlock = 1024 * kSegGroups;  // words per (client, item)
+__device__ __forceinline__ uint32_t seg_word(const SegPlan* pl, int nseg, int64_t total, int64_t w, int& k) {
+  int64_t pos = 32 * w;
+  const int64_t end = min(pos + 32, total);
+  uint32_t acc = 0;
+  while (pos < end) {
+    while (k < nseg && pos >= pl[k + 1].O) ++k;
+    while (k > 0 && pos < pl[k].O) --k;
+    const SegPlan& e = pl[k];
+    const int64_t rel = pos - e.O;
+    uint32_t n, bits;
+    if (k == nseg || rel < (int64_t)e.newR) {  // a new run code, or the trailing code
+      n = (uint32_t)min<int64_t>(end - pos, (int64_t)e.newR - rel);
+      bits = code_bits(e.dnew, e.newR, (uint32_t)rel, n);
+    } else {  // body bits, moved
+      n = (uint32_t)min<int64_t>(end - pos, e.len - rel);
+      const uint64_t sb = (uint64_t)e.srcbit + (uint64_t)(rel - e.newR);
+      const uint32_t* s32 = (const uint32_t*)e.src + (sb >> 5);
+      const uint32_t o = (uint32_t)(sb & 31);
+      uint32_t x = bswap32(s32[0]) << o;
+      if (o + n > 32) x |= bswap32(s32[1]) >> (32 - o);
+      bits = x >> (32 - n);
+    }
+    acc |= bits << (32 - (uint32_t)(pos - 32 * w) - n);
+    pos += n;
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void k_seg_copy(SegArgs a, int64_t blocks_per_client) {
+  __shared__ SegPlan pl[65];
+  __shared__ int64_t sh_total;
+  const int64_t items = blocks_per_client * a.nclients;
+  int cur = -1;
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const int c = (int)(it / blocks_per_client);
+    const int64_t w0 = (it - (int64_t)c * blocks_per_client) * kSegWordsPerBlock;
+    if (c != cur) {  // uniform across the workgroup
+      __syncthreads();
+      const SegPlan* src_pl = a.plan + (int64_t)c * (a.nseg + 1);
+      for (int i = threadIdx.x; i <= a.nseg; i += blockDim.x) pl[i] = src_pl[i];
+      if (threadIdx.x == 0) sh_total = a.overflow[c] ? 0 : src_pl[a.nseg].O + src_pl[a.nseg].len;
+      __syncthreads();
+      cur = c;
+    }
+    const int64_t total = sh_total;
+    const int64_t nwords = (total + 31) / 32;
+    // the first segment was coded in place: words before the one holding the second
+    // segment's first bit are final already (that word is read and rewritten by
+    // one thread: its first-segment bits come from the output itself)
+    const int64_t wstart = pl[1].O / 32;
+    if (w0 >= nwords || w0 + kSegWordsPerBlock <= wstart) continue;
+    uint32_t* out32 = (uint32_t*)(a.stream_buf + a.stream_off[c]);
+    const int64_t cap = a.stream_cap[c];
+    // kSegGroups groups of 4 words per thread, each group a coalesced 4-KiB block
+    // of the workgroup; every group's source loads are issued before any store
+    uint32_t x[kSegGroups][5];
+    uint32_t sh[kSegGroups];
+    uint32_t fast = 0;
+    int k = 0;
+#pragma unroll
+    for (int g = 0; g < kSegGroups; ++g) {
+      const int64_t w = w0 + 4 * threadIdx.x + 1024 * g;
+      if (w >= nwords || w + 4 <= wstart) continue;
+      while (k < a.nseg && 32 * w >= pl[k + 1].O) ++k;
+      const SegPlan& e = pl[k];
+      if (w >= wstart && k < a.nseg && 32 * w >= e.O + e.newR && 32 * (w + 4) <= e.O + e.len && (w + 4) * 4 <= cap) {
+        const uint64_t sb = (uint64_t)e.srcbit + (uint64_t)(32 * w - e.O - e.newR);
+        const uint32_t* s32 = (const uint32_t*)e.src + (sb >> 5);
+        sh[g] = (uint32_t)(sb & 31);
+#pragma unroll
+        for (int j = 0; j < 5; ++j) x[g][j] = s32[j];
+        fast |= 1u << g;
+      }
+    }
+    k = 0;
+#pragma unroll
+    for (int g = 0; g < kSegGroups; ++g) {
+      const int64_t w = w0 + 4 * threadIdx.x + 1024 * g;
+      if (w >= nwords || w + 4 <= wstart) continue;
+      if (fast & (1u << g)) {
+        const uint32_t o = sh[g];
+        uint32_t y[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) y[j] = bswap32(x[g][j]);
+        uint4 v;
+        v.x = bswap32(o ? (y[0] << o) | (y[1] >> (32 - o)) : y[0]);
+        v.y = bswap32(o ? (y[1] << o) | (y[2] >> (32 - o)) : y[1]);
+        v.z = bswap32(o ? (y[2] << o) | (y[3] >> (32 - o)) : y[2]);
+        v.w = bswap32(o ? (y[3] << o) | (y[4] >> (32 - o)) : y[3]);
+        *(uint4*)(out32 + w) = v;
+      } else {
+        for (int64_t ww = max(w, wstart); ww < min(nwords, w + 4); ++ww) {
+          const uint32_t v = seg_word(pl, a.nseg, total, ww, k);
+          if ((ww + 1) * 4 <= cap) out32[ww] = bswap32(v);
+        }
+      }
+    }
+  }
+}
+
+// The client's decoder index and per-tile measurement partials from its segments'.
+__global__ __launch_bounds__(256) void k_seg_index(SegArgs a) {
+  const int64_t T = (int64_t)a.K * a.Tv + (a.rem_elems > 0 ? a.Tr : 0);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)a.nclients * (T + 1)) return;
+  const int c = (int)(i / (T + 1));
+  const int64_t t = i - (int64_t)c * (T + 1);
+  const SegPlan* pl = a.plan + (int64_t)c * (a.nseg + 1);
+  if (t == T) {
+    a.idx[i] = ((uint64_t)pl[a.nseg].O & kMask36) | ((uint64_t)(pl[a.nseg].gprev + 1) << 36);
+    return;
+  }
+  const bool main = t < (int64_t)a.K * a.Tv;
+  const int k = main ? (int)(t / a.Tv) : a.K;
+  const int64_t j = main ? t - (int64_t)k * a.Tv : t - (int64_t)a.K * a.Tv;
+  const int64_t vrow = main ? ((int64_t)c * a.K + k) : c;
+  const uint64_t e = main ? a.vidx_main[vrow * (a.Tv + 1) + j] : a.vidx_rem[vrow * (a.Tr + 1) + j];
+  const int64_t vb = (int64_t)(e & kMask36), vl = (int64_t)(e >> 36) - 1;
+  const SegPlan& s = pl[k];
+  int64_t bits, last;
+  if (vl >= 0) {
+    bits = s.O + s.newR + (vb - (int64_t)s.srcbit);
+    last = (int64_t)k * a.seg_elems + vl;
+  } else {
+    bits = s.O;
+    last = s.gprev;
+  }
+  a.idx[i] = ((uint64_t)bits & kMask36) | ((uint64_t)(last + 1) << 36);
+  const int64_t d = (int64_t)c * T + t;
+  if (a.dist_part) a.dist_part[d] = main ? a.vdist_main[vrow * a.Tv + j] : a.vdist_rem[vrow * a.Tr + j];
+  if (a.nnz_part) a.nnz_part[d] = main ? a.vnnz_main[vrow * a.Tv + j] : a.vnnz_rem[vrow * a.Tr + j];
+}
+
+struct SegLayout {
+  int64_t seg_elems, rem_elems, nv, vcap_main, vcap_rem;
+  int32_t Tv, Tr, nseg;
+  int64_t o_ws_main, o_ws_rem, o_vptr, o_voff, o_vseeds, o_vnorms, o_vpre, o_vsoff, o_vscap, o_vidx_main,
+      o_vidx_rem, o_vbits, o_vdist_main, o_vdist_rem, o_vnnz_main, o_vnnz_rem, o_vovf, o_plan, o_vstream, total;
+};
+
+// Workspace layout of fc_quantize_encode_segmented (every piece 256-B aligned).
+// Returns false if the segmentation is not possible (segments below 2048 elements).
+bool seg_layout(int32_t C, int64_t P, int32_t K, int64_t max_cap, SegLayout& L) {
+  if (C <= 0 || K < 1 || K > 63 || P <= 0 || max_cap <= 0) return false;
+  L.seg_elems = P / K / 2048 * 2048;
+  if (L.seg_elems < 2048) return false;
+  L.rem_elems = P - (int64_t)K * L.seg_elems;
+  L.Tv = (int32_t)tiles_for(L.seg_elems);
+  L.Tr = L.rem_elems > 0 ? (int32_t)tiles_for(L.rem_elems) : 0;
+  L.nseg = K + (L.rem_elems > 0 ? 1 : 0);
+  const int64_t nmain = (int64_t)C * K, nrem = L.rem_elems > 0 ? C : 0;
+  L.nv = nmain + nrem;
+  // a segment's code needs at most its share of the client's capacity, plus slack
+  // for the first run code and the per-segment trailing code
+  L.vcap_main = (max_cap * L.seg_elems / P + 8192 + 255) / 256 * 256;
+  L.vcap_rem = nrem ? (max_cap * L.rem_elems / P + 8192 + 255) / 256 * 256 : 0;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    const int64_t r = o;
+    o += (bytes + 255) / 256 * 256;
+    return r;
+  };
+  L.o_ws_main = take(enc_workspace_bytes((int32_t)nmain, L.seg_elems));
+  L.o_ws_rem = take(nrem ? enc_workspace_bytes(C, L.rem_elems) : 0);
+  L.o_vptr = take(8 * L.nv);
+  L.o_voff = take(8 * L.nv);
+  L.o_vseeds = take(16 * L.nv);
+  L.o_vnorms = take(4 * L.nv);
+  L.o_vpre = take(8 * L.nv);
+  L.o_vsoff = take(8 * L.nv);
+  L.o_vscap = take(8 * L.nv);
+  L.o_vidx_main = take(8 * nmain * (L.Tv + 1));
+  L.o_vidx_rem = take(8 * nrem * (L.Tr + 1));
+  L.o_vbits = take(8 * L.nv);
+  L.o_vdist_main = take(4 * nmain * L.Tv);
+  L.o_vdist_rem = take(4 * nrem * L.Tr);
+  L.o_vnnz_main = take(4 * nmain * L.Tv);
+  L.o_vnnz_rem = take(4 * nrem * L.Tr);
+  L.o_vovf = take(4 * L.nv);
+  L.o_plan = take((int64_t)sizeof(SegPlan) * C * (L.nseg + 1));
+  L.o_vstream = take(nmain * L.vcap_main + nrem * L.vcap_rem + 64);
+  L.total = o;
+  return true;
+}
+
+int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float step, const float* norms,
+                     const float* prescale, const int64_t* seeds, int mode, int32_t K, int64_t max_cap,
+                     uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
+                     int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow, void* workspace,
+                     int64_t workspace_bytes, void* stream) {
+  SegLayout L;
+  if (!seg_layout(nclients, P, K, max_cap, L)) return fail(-1, "segmented encode: segments below 2048 elements");
+  if (!xs || !stream_buf || !stream_off || !stream_cap || !idx || !total_bits || !overflow)
+    return fail(-1, "null required pointer");
+  if (!workspace || workspace_bytes < L.total || ((uintptr_t)workspace & 255))
+    return fail(-1, "segmented workspace too small or not 256-byte aligned");
+  uint8_t* w = (uint8_t*)workspace;
+  SegArgs a;
+  a.xs = (const void* const*)xs;
+  a.nclients = nclients;
+  a.K = K;
+  a.nseg = L.nseg;
+  a.P = P;
+  a.seg_elems = L.seg_elems;
+  a.rem_elems = L.rem_elems;
+  a.Tv = L.Tv;
+  a.Tr = L.Tr;
+  a.norms = norms;
+  a.prescale = prescale;
+  a.seeds = seeds;
+  a.vptr = (const float**)(w + L.o_vptr);
+  a.voff = (int64_t*)(w + L.o_voff);
+  a.vseeds = (int64_t*)(w + L.o_vseeds);
+  a.vnorms = (float*)(w + L.o_vnorms);
+  a.vpre = (float*)(w + L.o_vpre);
+  a.vstream_off = (int64_t*)(w + L.o_vsoff);
+  a.vstream_cap = (int64_t*)(w + L.o_vscap);
+  a.vstream = w + L.o_vstream;
+  a.vcap_main = L.vcap_main;
+  a.vcap_rem = L.vcap_rem;
+  a.vidx_main = (uint64_t*)(w + L.o_vidx_main);
+  a.vidx_rem = (uint64_t*)(w + L.o_vidx_rem);
+  a.vbits = (int64_t*)(w + L.o_vbits);
+  a.vdist_main = (float*)(w + L.o_vdist_main);
+  a.vdist_rem = (float*)(w + L.o_vdist_rem);
+  a.vnnz_main = (int32_t*)(w + L.o_vnnz_main);
+  a.vnnz_rem = (int32_t*)(w + L.o_vnnz_rem);
+  a.vovf = (int32_t*)(w + L.o_vovf);
+  a.plan = (SegPlan*)(w + L.o_plan);
+  a.stream_buf = stream_buf;
+  a.stream_off = stream_off;
+  a.stream_cap = stream_cap;
+  a.idx = idx;
+  a.total_bits = total_bits;
+  a.dist_part = dist_part;
+  a.nnz_part = nnz_part;
+  a.overflow = overflow;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_seg_setup, dim3((unsigned)((L.nv + 255) / 256)), dim3(256), 0, s, a);
+  if (const int rc = check_launch("k_seg_setup")) return rc;
+  const int32_t nmain = nclients * K;
+  int rc = encode_common((const void* const*)a.vptr, nmain, L.seg_elems, step, norms ? a.vnorms : nullptr,
+                         prescale ? a.vpre : nullptr, seeds ? a.vseeds : nullptr, mode, false, a.vstream,
+                         a.vstream_off, a.vstream_cap, a.vidx_main, a.vbits, a.vdist_main, a.vnnz_main, a.vovf,
+                         w + L.o_ws_main, L.o_ws_rem - L.o_ws_main, stream, a.voff);
+  if (rc) return rc;
+  if (L.rem_elems > 0) {
+    rc = encode_common((const void* const*)(a.vptr + nmain), nclients, L.rem_elems, step,
+                       norms ? a.vnorms + nmain : nullptr, prescale ? a.vpre + 2 * (int64_t)nmain : nullptr,
+                       seeds ? a.vseeds + 2 * (int64_t)nmain : nullptr, mode, false, a.vstream, a.vstream_off + nmain,
+                       a.vstream_cap + nmain, a.vidx_rem, a.vbits + nmain, a.vdist_rem, a.vnnz_rem, a.vovf + nmain,
+                       w + L.o_ws_rem, L.o_vptr - L.o_ws_rem, stream, a.voff + nmain);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(k_seg_plan, dim3(nclients), dim3(64), 0, s, a);
+  if (const int rc2 = check_launch("k_seg_plan")) return rc2;
+  const int64_t bpc = (max_cap / 4 + kSegWordsPerBlock - 1) / kSegWordsPerBlock;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t cgrid = std::min<int64_t>(bpc * nclients, (int64_t)ncu * 16);
+  hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)cgrid), dim3(256), 0, s, a, bpc);
+  if (const int rc3 = check_launch("k_seg_copy")) return rc3;
+  const int64_t T = tiles_for(P);
+  hipLaunchKernelGGL(k_seg_index, dim3((unsigned)(((int64_t)nclients * (T + 1) + 255) / 256)), dim3(256), 0, s, a);
+  return check_launch("k_seg_index");
+}
+
 // QSGD decode: client q rows per group at most this many bytes (fc_decode_scaled_workspace_bytes).
 constexpr int64_t kScaledPlaneBudget = 1LL << 30;
 
@@ -3688,6 +4177,24 @@ int fc_quantize_encode(const float* const* xs, int32_t nclients, int64_t P, floa
   return encode_common((const void* const*)xs, nclients, P, step, norms, prescale, seeds, mode, false, stream_buf,
                        stream_off, stream_cap, idx, total_bits, dist_part, nnz_part, overflow, workspace,
                        workspace_bytes, stream);
+}
+
+int64_t fc_segmented_workspace_bytes(int32_t nclients, int64_t P, int32_t nseg, int64_t max_cap) {
+  SegLayout L;
+  if (!seg_layout(nclients, P, nseg, max_cap, L)) return -1;
+  return L.total;
+}
+
+int fc_quantize_encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float step,
+                                 const float* norms, const float* prescale, const int64_t* seeds, int mode,
+                                 int32_t nseg, int64_t max_cap, uint8_t* stream_buf, const int64_t* stream_off,
+                                 const int64_t* stream_cap, uint64_t* idx, int64_t* total_bits, float* dist_part,
+                                 int32_t* nnz_part, int32_t* overflow, void* workspace, int64_t workspace_bytes,
+                                 void* stream) {
+  if (mode < 0 || mode > 2) return fail(-1, "mode must be 0 (uniform), 1 (stochastic) or 2 (dithered)");
+  return encode_segmented(xs, nclients, P, step, norms, prescale, seeds, mode, nseg, max_cap, stream_buf, stream_off,
+                          stream_cap, idx, total_bits, dist_part, nnz_part, overflow, workspace, workspace_bytes,
+                          stream);
 }
 
 int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P, uint8_t* stream_buf,

@@ -112,6 +112,27 @@ int fc_quantize_encode(const float* const* xs, int32_t nclients, int64_t P, floa
                        float* dist_part, int32_t* nnz_part, int32_t* overflow,
                        void* workspace, int64_t workspace_bytes, void* stream);
 
+/* Segmented quantise + encode (few clients per GPU; same results as
+ * fc_quantize_encode, bit for bit).  Each client is cut into nseg element
+ * segments (a multiple of 2048 elements each, plus a remainder) encoded as
+ * independent rows -- each continuing its client's Philox stream -- then
+ * stitched into the client's canonical stream (first run codes rebased on the
+ * client's previous nonzero, per-segment trailing codes dropped, bits moved),
+ * with the decoder index and the measurement partials rebased.  max_cap: the
+ * largest stream_cap (sizes the segments' staging).  Workspace:
+ * fc_segmented_workspace_bytes (256-byte aligned); -1 there means the
+ * segmentation is not possible (segments under 2048 elements).  Replaces the
+ * same reference call as fc_quantize_encode (quantize_encode.py:139-156 +
+ * elias_gamma_encode.py:97-99). */
+int64_t fc_segmented_workspace_bytes(int32_t nclients, int64_t P, int32_t nseg, int64_t max_cap);
+int fc_quantize_encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float step,
+                                 const float* norms, const float* prescale, const int64_t* seeds,
+                                 int mode, int32_t nseg, int64_t max_cap, uint8_t* stream_buf,
+                                 const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
+                                 int64_t* total_bits, float* dist_part, int32_t* nnz_part,
+                                 int32_t* overflow, void* workspace, int64_t workspace_bytes,
+                                 void* stream);
+
 /* tfc.run_length_gamma_encode over int32 inputs (same batch layout as above,
  * qs = device array of device pointers to int32[P]). */
 int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P,
