@@ -83,7 +83,9 @@ def parse():
   ap.add_argument("--sigma", type=float, default=1.0)
   ap.add_argument("--pool", type=int, default=0,
                   help="distinct delta buffers cycled over clients (0 = one per client)")
-  ap.add_argument("--cap-bytes-per-elem", type=float, default=1.0)
+  ap.add_argument("--cap-bytes-per-elem", type=float, default=0.0,
+                  help="stream capacity per element; 0: sized as QuantizeEncodeFactory does "
+                       "(codec.CapacityHint from an untimed probe round)")
   ap.add_argument("--no-cpu-baseline", action="store_true")
   ap.add_argument("--cpu-sample-clients", type=int, default=32)
   ap.add_argument("--dump-result", default="",
@@ -234,6 +236,22 @@ def roofline(kernel, alg_bytes, launch_ms, workload):
           "alg_bytes_per_launch": alg_bytes, "launch_ms": round(launch_ms, 3)}
 
 
+def sized_batch(P, C, dev, encode, cap_per_elem=0.0):
+  """The round's EncodedBatch with capacities as the factory sizes them: an
+  untimed probe encode (1 byte per element), then codec.CapacityHint (largest
+  client code + 1/8 + 4 KiB) -- what QuantizeEncodeFactory uses from its second
+  round on.  cap_per_elem > 0: that fixed capacity instead."""
+  if cap_per_elem > 0:
+    return codec.EncodedBatch(P, C, [codec._round_up(int(P * cap_per_elem) + 256, 64)] * C, dev)  # pylint: disable=protected-access
+  probe = codec.EncodedBatch(P, C, [codec._round_up(P + 256, 64)] * C, dev)  # pylint: disable=protected-access
+  encode(probe)
+  hint = codec.CapacityHint()
+  hint.update(probe)
+  del probe
+  torch.cuda.empty_cache()
+  return codec.EncodedBatch(P, C, hint.caps(P, C), dev)
+
+
 def make_deltas(C, P, sigma, dev, seed0):
   g = torch.Generator(device=dev)
   rows = []
@@ -243,13 +261,13 @@ def make_deltas(C, P, sigma, dev, seed0):
   return rows
 
 
-def codec_round(name, rows, ptrs, P, step, mode, steps, warmup, stream, cap_per_elem=1.0, workload=None):
+def codec_round(name, rows, ptrs, P, step, mode, steps, warmup, stream, workload=None):
   """Encode + decode + dequantise rounds of one codec configuration; HIP-event timed."""
   C = len(rows)
   dev = rows[0].device
   seeds = torch.tensor([[500 + c, 500 + c] for c in range(C)], dtype=torch.int64, device=dev)
-  cap = codec._round_up(int(P * cap_per_elem) + 256, 64)  # pylint: disable=protected-access
-  batch = codec.EncodedBatch(P, C, [cap] * C, dev)
+  batch = sized_batch(P, C, dev, lambda b: codec.quantize_encode(None, step, seeds, mode, ptrs=ptrs, P=P, out=b,
+                                                                  stream=stream))
   out = torch.empty(P, dtype=torch.float32, device=dev)
   err = torch.zeros(1, dtype=torch.int32, device=dev)
   tm = Timer(stream)
@@ -286,8 +304,7 @@ def w_trainer_round(rows, ptrs, P, steps, warmup, stream):
   step = 0.5
   w = torch.arange(200, 200 + C, dtype=torch.float32)  # example counts
   seeds = torch.tensor([[9 + c, 9 + c] for c in range(C)], dtype=torch.int64, device=dev)
-  cap = codec._round_up(P + 256, 64)  # pylint: disable=protected-access
-  batch = codec.EncodedBatch(P, C, [cap] * C, dev)
+  batch = None  # sized by the first round (below)
   out = torch.empty(P, dtype=torch.float32, device=dev)
   err = torch.zeros(1, dtype=torch.int32, device=dev)
   denom = torch.full((1,), float(w.sum()), dtype=torch.float32, device=dev)
@@ -313,6 +330,9 @@ def w_trainer_round(rows, ptrs, P, steps, warmup, stream):
       inv = np.where(l2 > 0, np.float32(1.0) / l2, np.float32(np.inf)).astype(np.float32)
     s0 = np.where(keep, clip * np.minimum(inv, np.float32(1.0) / clip), np.float32(0.0)).astype(np.float32)
     pre = torch.from_numpy(np.stack([s0, w.numpy()], 1).astype(np.float32)).to(dev, non_blocking=True)
+    if batch is None:
+      batch = sized_batch(P, C, dev, lambda b: codec.quantize_encode(None, step, seeds, _lib.UNIFORM, ptrs=ptrs, P=P,
+                                                                      out=b, stream=stream, prescale=pre))
     t.phase("k_encode", lambda: codec.quantize_encode(None, step, seeds, _lib.UNIFORM, ptrs=ptrs, P=P, out=batch,
                                                       stream=stream, prescale=pre))
     t.phase("k_decode", lambda: codec.decode_accumulate(batch, want_sum=False, out=out, step=step, err=err,
@@ -407,8 +427,7 @@ def run_extra(name, args, dev, stream, head_rows, head_ptrs):
     rows = make_deltas(256, 4_050_748, 1.0, dev, 9000)
     step = 1.0
   ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
-  r = codec_round(name, rows, ptrs, rows[0].numel(), step, _lib.STOCHASTIC, max(steps, 10), warmup, stream,
-                  cap_per_elem=2.5 if name == "config2" else 1.0)
+  r = codec_round(name, rows, ptrs, rows[0].numel(), step, _lib.STOCHASTIC, max(steps, 10), warmup, stream)
   del rows
   return r
 
@@ -529,8 +548,8 @@ def main():
 
   base = 1000 + rank * Cg
   seeds = torch.tensor([[base + c, base + c] for c in range(Cg)], dtype=torch.int64, device=dev)
-  cap = codec._round_up(int(P * args.cap_bytes_per_elem) + 256, 64)  # pylint: disable=protected-access
-  batch = codec.EncodedBatch(P, Cg, [cap] * Cg, dev)
+  batch = sized_batch(P, Cg, dev, lambda b: codec.quantize_encode(None, args.step_size, seeds, mode, ptrs=ptrs, P=P,
+                                                                   out=b, stream=stream), args.cap_bytes_per_elem)
   out = torch.empty(P, dtype=torch.float32, device=dev)
   isum = torch.empty(P, dtype=torch.int32, device=dev)
   err = torch.zeros(1, dtype=torch.int32, device=dev)

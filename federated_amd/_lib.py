@@ -29,6 +29,8 @@ SIGNATURES = {
     "fc_quantize_encode": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P,
                                   _P, _P, _P, _P, _I64, _P]),
     "fc_rlgamma_encode": (_INT, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "fc_quantize_encode_hinted": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P,
+                                         _P, _P, _P, _P, _I64, _I64, _P]),
     "fc_segmented_workspace_bytes": (_I64, [_I32, _I64, _I32, _I64]),
     "fc_quantize_encode_segmented": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _I32, _I64, _P, _P, _P, _P,
                                             _P, _P, _P, _P, _P, _I64, _P]),

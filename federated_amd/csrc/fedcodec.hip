@@ -1740,6 +1740,9 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
 #define FC_WIN2_WORDS (2 * FC_WIN_WORDS)
 #endif
 constexpr uint32_t kWin2Words = FC_WIN2_WORDS;
+// four-tile tickets while codes are expected within this many bits per element
+// (their window holds 32 * kWin2Words - kPre - 96 bits = ~8.4 bits per element)
+constexpr double kNt4Bits = 6.5;
 constexpr int kSTE = 2 * kTE;  // elements per super-tile
 
 // LDS-DMA of one full, 16-B-aligned tile into the staging (as stage_tile).
@@ -1766,8 +1769,12 @@ constexpr int kEnc2Waves = 4;
 #ifndef FC_PAIR_LUT
 #define FC_PAIR_LUT 1
 #endif
-template <int MODE, bool INT_IN, int DIV, bool PRE>
+#ifndef FC_LB_LATE
+#define FC_LB_LATE 0  // k_encode2: look-back window loaded after the last tile's codes (A/B knob)
+#endif
+template <int MODE, bool INT_IN, int DIV, bool PRE, int NT>
 __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_encode2(EncodeArgs a) {
+  constexpr int STE = NT * kTE;  // elements per super-tile (ticket)
   __shared__ uint32_t wins[kEnc2Waves][kWin2Words + 3];  // + guard words
   __shared__ uint32_t clut[kCodeLut];
   __shared__ uint32_t plut[kPairLut];
@@ -1797,16 +1804,21 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
   if (ticket < total) {
     const int32_t t2 = (int32_t)div_clients(a, ticket);
     const int32_t c = (int32_t)(ticket - (uint32_t)t2 * (uint32_t)a.nclients);
-    staged = stage_at(cparams[c].x, (int64_t)t2 * kSTE, P, stg, lane);
+    staged = stage_at(cparams[c].x, (int64_t)t2 * STE, P, stg, lane);
   }
   __builtin_amdgcn_s_waitcnt(kWaitVm0);
+#ifdef FC_STAMPS
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
 
   while (ticket < total) {
+    STAMP(7);
     const int32_t t2 = (int32_t)div_clients(a, ticket);
     const int32_t c = (int32_t)(ticket - (uint32_t)t2 * (uint32_t)a.nclients);
-    const int32_t t0 = 2 * t2;  // first tile of the super-tile
-    const bool has1 = t0 + 1 < a.T;
-    const int64_t sbase = (int64_t)t2 * kSTE;
+    const int32_t t0 = NT * t2;  // first tile of the super-tile
+    const int nt = min(NT, a.T - t0);  // tiles in this super-tile
+    const int64_t sbase = (int64_t)t2 * STE;
     // the client's parameters: the quantiser and row here, the stream at the end
     // (re-read there: fewer scalar registers held across the two tiles)
     const ClientQ cq = client_q_of(ld_param(cparams + c), PRE);
@@ -1816,18 +1828,22 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     float dist = 0.0f;
     int32_t nnz = 0;  // INT_IN: per lane; float input: wave total
     uint32_t lng = 0;  // lane has a long chunk (either tile)
-    uint32_t body = 0, body0 = 0;
-    int32_t sfirst = -1, slast = -1, last0 = -1;  // super-tile-relative first / last nonzero
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1) {
-        if (!has1) break;
+    uint32_t body = 0;
+    int32_t sfirst = -1, slast = -1;  // super-tile-relative first / last nonzero
+    uint32_t bodyb[NT];   // body bits before tile h
+    int32_t lastb[NT];    // last nonzero before tile h (super-tile-relative, -1 none)
+    for (int h = 0; h < NT; ++h) {
+      if (h >= 1) {
+        if (h >= nt) break;
+        STAMP(0);
         __builtin_amdgcn_s_waitcnt(kWaitVm0);  // the second tile's staging has landed
+        STAMP(1);
       }
       const int64_t tile_base = sbase + (int64_t)h * kTE;
       const bool full = tile_base + kTE <= P;
       const int32_t lrel = 16 * lane;
       uint32_t raw[kChunks][4];
-      if (!staged) {  // a client's last (partial) tile or an unaligned row: load into the staging
+      if (!staged && !(FC_ABL & 64)) {  // a client's last (partial) tile or an unaligned row: load into the staging
 #pragma unroll
         for (int j = 0; j < kChunks; ++j) {
           const int64_t e0 = tile_base + lrel + 4 * j;
@@ -1849,21 +1865,30 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      // the staging is free once read: stage this super-tile's second tile, or the
+      if (FC_ABL & 64) {  // diagnostics: synthetic values in [-2, 2), no input loads
+#pragma unroll
+        for (int j = 0; j < kChunks; ++j)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t hsh = ((uint32_t)tile_base + 16u * (uint32_t)lane + 4u * j + k) * 2654435761u ^ (uint32_t)c;
+            raw[j][k] = __float_as_uint(__uint_as_float((hsh & 0x7FFFFFu) | 0x40000000u) - 3.0f);
+          }
+      }
+      // the staging is free once read: stage this super-tile's next tile, or the
       // next super-tile's first (waited for before it is read)
-      if (h == 0 && has1) {
+      if (h + 1 < nt) {
         staged = stage_at(xrow, tile_base + kTE, P, stg, lane);
       } else {
         staged = false;
         if (ticket1 < total) {
           const int32_t n2 = (int32_t)div_clients(a, ticket1);
           const int32_t nc = (int32_t)(ticket1 - (uint32_t)n2 * (uint32_t)a.nclients);
-          staged = stage_at(cparams[nc].x, (int64_t)n2 * kSTE, P, stg, lane);
+          staged = stage_at(cparams[nc].x, (int64_t)n2 * STE, P, stg, lane);
           // the ticket after next: its round trip completes under this tile's work
           if (lane == 0) ntk = atomicAdd(my_counter, 1u);
         }
         // the look-back window, loaded under the last tile's work
-        if (t2 + lane >= 64 && lane >= a.lb_lane0) {
+        if (!FC_LB_LATE && t2 + lane >= 64 && lane >= a.lb_lane0) {
           const uint64_t* sp = a.status + 2 * ((int64_t)c * a.T + t2 - 64 + lane);
           pw1 = ld_agent(sp);
           pw2 = ld_agent(sp + 1);
@@ -1905,6 +1930,15 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         llen += cc.len;
         FC_CHUNK_BARRIER;
       }
+      STAMP(2);
+      // the look-back window, loaded late (FC_LB_LATE): after the last tile's codes,
+      // so the statuses of predecessors still coding when the tile began are
+      // more likely published (fewer re-polls), under the scans and emission
+      if (FC_LB_LATE && h + 1 >= nt && t2 + lane >= 64 && lane >= a.lb_lane0) {
+        const uint64_t* sp = a.status + 2 * ((int64_t)c * a.T + t2 - 64 + lane);
+        pw1 = ld_agent(sp);
+        pw2 = ld_agent(sp + 1);
+      }
       // ---- B: scans -- last nonzero before each lane (lane 0: the first half's
       //      last nonzero, or none), then code offsets after the bits so far
       const int32_t im = dpp_incl_max(max(llast, slast));  // slast < every position of this tile
@@ -1917,7 +1951,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       const uint32_t is = dpp_incl_sum(ltot);
       const uint32_t hbody = (uint32_t)lane63((int32_t)is);
       // ---- C: emit the lane's run code and chunks
-      {
+      if (!(FC_ABL & 1)) {  // (diagnostics: no emission)
         uint32_t o = kPre + body + is - ltot;
         emit32<kWin2Words>(win, dv, R, o);
         o += R;
@@ -1939,14 +1973,14 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         const uint64_t fm = __ballot(lfirst >= 0);  // lanes are in element order
         sfirst = fm ? __builtin_amdgcn_readlane(lfirst, (int)__builtin_ctzll(fm)) : -1;
       }
+      bodyb[h] = body;
+      lastb[h] = slast;
       slast = hlast >= 0 ? hlast : slast;
       body += hbody;
-      if (h == 0) {
-        body0 = hbody;
-        last0 = hlast;
-      }
     }
+    STAMP(3);
     __builtin_amdgcn_s_waitcnt(kWaitVm0);  // next tile staged, look-back window loaded
+    STAMP(4);
     // fast path: no long chunk, prefix + body + trailing code + one funnel word fit
     // the window, and a finite distortion (no NaN / infinite r)
     const float dsum = INT_IN ? 0.0f : wave_sum_f(dist);
@@ -1959,11 +1993,11 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       if (lane == 0) {  // one partial per super-tile (its second tile's slot: 0)
         if (a.dist_part) {
           a.dist_part[(int64_t)c * a.T + t0] = d;
-          if (has1) a.dist_part[(int64_t)c * a.T + t0 + 1] = 0.0f;
+          for (int h = 1; h < nt; ++h) a.dist_part[(int64_t)c * a.T + t0 + h] = 0.0f;
         }
         if (a.nnz_part) {
           a.nnz_part[(int64_t)c * a.T + t0] = n;
-          if (has1) a.nnz_part[(int64_t)c * a.T + t0 + 1] = 0;
+          for (int h = 1; h < nt; ++h) a.nnz_part[(int64_t)c * a.T + t0 + h] = 0;
         }
       }
     }
@@ -1977,7 +2011,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     bool slow = !fast;
     Seg excl = seg_identity();
     if (fast) {
-      if (t2 == 0) {  // chain root: the inclusive prefix right away
+      if (t2 == 0 || (FC_ABL & 4)) {  // chain root: the inclusive prefix right away (diagnostics: every super-tile)
         excl.has_nz = 1;
         excl.first = excl.last = -1;
         if (lane == 0) {
@@ -1992,7 +2026,9 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           st_agent(st + 1, kFlagAgg | agg_tail);
           st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
         }
-        excl = lookback_vec<kSTE>(a.status + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2);
+        STAMP(5);
+        excl = lookback_vec<STE>(a.status + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2);
+        STAMP(6);
       }
     }
     if (slow) {
@@ -2029,10 +2065,12 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         }
         const int64_t ib = (int64_t)c * (a.T + 1);
         a.idx[ib + t0] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
-        if (has1) {  // the second tile: after the first's code (and the run code before it)
-          const uint64_t off = excl.body + (last0 >= 0 ? (uint64_t)R0 + body0 : 0u);
-          const int32_t lb = last0 >= 0 ? (int32_t)(sbase + last0) : excl.last;
-          a.idx[ib + t0 + 1] = (off & kMask36) | ((uint64_t)(lb + 1) << 36);
+#pragma unroll
+        for (int h = 1; h < NT; ++h) {  // later tiles: after the earlier tiles' codes (and the run code before them)
+          if (h >= nt) break;
+          const uint64_t off = excl.body + (lastb[h] >= 0 ? (uint64_t)R0 + bodyb[h] : 0u);
+          const int32_t lb = lastb[h] >= 0 ? (int32_t)(sbase + lastb[h]) : excl.last;
+          a.idx[ib + t0 + h] = (off & kMask36) | ((uint64_t)(lb + 1) << 36);
         }
         if (last_st) {
           a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
@@ -2053,7 +2091,8 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
       for (uint32_t k = lane; k < nwords_owned; k += kEncThreads) {
         const uint32_t wv32 = win_bits32(win, s0 + 32 * k);
-        if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
+        if (FC_ABL & 2) asm volatile("" :: "v"(wv32));  // diagnostics: no stream stores
+        else if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
       }
       const uint32_t nt = min(kWin2Words, (kPre + body + trail_len + 31) / 32 + 1);
       for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
@@ -2061,6 +2100,10 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     ticket = ticket1;
     if (ticket1 < total) ticket1 = shard + a.nshards * uniform(ntk);
   }
+#ifdef FC_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_stamps[i], (unsigned long long)st_acc[i]);
+#endif
 }
 
 // Reset the look-back status (and overflow flag) of the clients k_encode
@@ -3486,7 +3529,8 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
                   const float* prescale, const int64_t* seeds, int mode, bool int_in, uint8_t* stream_buf,
                   const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
                   int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow,
-                  void* workspace, int64_t workspace_bytes, void* stream, const int64_t* elem_off = nullptr) {
+                  void* workspace, int64_t workspace_bytes, void* stream, const int64_t* elem_off = nullptr,
+                  int64_t max_cap = 0) {
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
   if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
   if (!xs || !stream_buf || !stream_off || !stream_cap || !idx || !total_bits || !overflow)
@@ -3550,10 +3594,12 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   a.rcp = (pow2 || mark) ? 1.0f / step : 0.0f;
   void (*kern)(EncodeArgs) = nullptr;
   void (*kern2)(EncodeArgs) = nullptr;
+  void (*kern4)(EncodeArgs) = nullptr;
   void (*exact)(EncodeArgs) = nullptr;
   const bool pre = !int_in && prescale != nullptr;
-#define FC_PICK(M, I, D, Q) \
-  (kern = k_encode<M, I, D, Q>, kern2 = k_encode2<M, I, D, Q>, exact = k_encode_exact<M, I, D == 1>)
+#define FC_PICK(M, I, D, Q)                                                                       \
+  (kern = k_encode<M, I, D, Q>, kern2 = k_encode2<M, I, D, Q, 2>, kern4 = k_encode2<M, I, D, Q, 4>, \
+   exact = k_encode_exact<M, I, D == 1>)
 #define FC_PICK2(M, D) (pre ? FC_PICK(M, false, D, true) : FC_PICK(M, false, D, false))
 #define FC_PICK3(M) (pow2 ? FC_PICK2(M, 1) : mark ? FC_PICK2(M, 2) : FC_PICK2(M, 0))
   if (int_in) FC_PICK(FC_UNIFORM, true, 0, false);
@@ -3581,7 +3627,18 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
     per_cu0 = 1;
   bool super = (int64_t)ncu * per_cu0 * kEnc2Waves <= 4LL * nclients && T >= 2;
   if (const char* e = getenv("FEDCODEC_ENC2")) super = atoi(e) != 0;  // test knob
-  if (super) kern = kern2;
+  // four tiles per ticket (FEDCODEC_ENC_NT=4): the per-ticket work (ticket, status,
+  // look-back, reductions, store set-up) paid once per 4096 elements; the window
+  // (the same LDS) then holds about 8.4 bits per element before the exact path
+  // by the caller's largest stream capacity (host-known): codes expected within
+  // kNt4Bits bits per element (+ slack) take four-tile tickets; denser ones, or an
+  // unknown capacity, two (a window overflow sends the client to the exact path)
+  int nt = (max_cap > 0 && 8.0 * (double)max_cap <= kNt4Bits * (double)P + 8.0 * 8192.0) ? 4 : 2;
+  if (const char* e = getenv("FEDCODEC_ENC_NT")) nt = atoi(e) == 4 ? 4 : 2;  // test knob
+  if (super) {
+    kern = nt == 4 ? kern4 : kern2;
+    a.T2 = (int32_t)((T + nt - 1) / nt);
+  }
   const int wpg = super ? kEnc2Waves : 1;  // waves per workgroup
   const int64_t tickets = super ? (int64_t)nclients * a.T2 : total;
   // Persistent grid no larger than what is co-resident (every ticket stream has a
@@ -4056,14 +4113,16 @@ int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float 
   int rc = encode_common((const void* const*)a.vptr, nmain, L.seg_elems, step, norms ? a.vnorms : nullptr,
                          prescale ? a.vpre : nullptr, seeds ? a.vseeds : nullptr, mode, false, a.vstream,
                          a.vstream_off, a.vstream_cap, a.vidx_main, a.vbits, a.vdist_main, a.vnnz_main, a.vovf,
-                         w + L.o_ws_main, L.o_ws_rem - L.o_ws_main, stream, a.voff);
+                         w + L.o_ws_main, L.o_ws_rem - L.o_ws_main, stream, a.voff,
+                         std::min(L.vcap_main, max_cap * L.seg_elems / P + 8192));
   if (rc) return rc;
   if (L.rem_elems > 0) {
     rc = encode_common((const void* const*)(a.vptr + nmain), nclients, L.rem_elems, step,
                        norms ? a.vnorms + nmain : nullptr, prescale ? a.vpre + 2 * (int64_t)nmain : nullptr,
                        seeds ? a.vseeds + 2 * (int64_t)nmain : nullptr, mode, false, a.vstream, a.vstream_off + nmain,
                        a.vstream_cap + nmain, a.vidx_rem, a.vbits + nmain, a.vdist_rem, a.vnnz_rem, a.vovf + nmain,
-                       w + L.o_ws_rem, L.o_vptr - L.o_ws_rem, stream, a.voff + nmain);
+                       w + L.o_ws_rem, L.o_vptr - L.o_ws_rem, stream, a.voff + nmain,
+                       max_cap * L.rem_elems / P + 8192);
     if (rc) return rc;
   }
   hipLaunchKernelGGL(k_seg_plan, dim3(nclients), dim3(64), 0, s, a);
@@ -4081,6 +4140,7 @@ int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float 
 }
 
 // QSGD decode: client q rows per group at most this many bytes (fc_decode_scaled_workspace_bytes).
+
 constexpr int64_t kScaledPlaneBudget = 1LL << 30;
 
 // Shared launcher of k_decode (int32 client sum, or the q rows of a client group).
@@ -4195,6 +4255,17 @@ int fc_quantize_encode_segmented(const float* const* xs, int32_t nclients, int64
   return encode_segmented(xs, nclients, P, step, norms, prescale, seeds, mode, nseg, max_cap, stream_buf, stream_off,
                           stream_cap, idx, total_bits, dist_part, nnz_part, overflow, workspace, workspace_bytes,
                           stream);
+}
+
+int fc_quantize_encode_hinted(const float* const* xs, int32_t nclients, int64_t P, float step,
+                              const float* norms, const float* prescale, const int64_t* seeds, int mode,
+                              uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap,
+                              uint64_t* idx, int64_t* total_bits, float* dist_part, int32_t* nnz_part,
+                              int32_t* overflow, void* workspace, int64_t workspace_bytes, int64_t max_cap,
+                              void* stream) {
+  return encode_common((const void* const*)xs, nclients, P, step, norms, prescale, seeds, mode, false, stream_buf,
+                       stream_off, stream_cap, idx, total_bits, dist_part, nnz_part, overflow, workspace,
+                       workspace_bytes, stream, nullptr, max_cap);
 }
 
 int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P, uint8_t* stream_buf,

@@ -112,6 +112,20 @@ int fc_quantize_encode(const float* const* xs, int32_t nclients, int64_t P, floa
                        float* dist_part, int32_t* nnz_part, int32_t* overflow,
                        void* workspace, int64_t workspace_bytes, void* stream);
 
+/* fc_quantize_encode with a host-side hint: max_cap = the largest stream_cap[c]
+ * (bytes; <= 0 unknown).  Same results bit for bit; the hint picks the encoder's
+ * ticket size: codes expected within 6.5 bits per element take four-tile
+ * tickets (per-ticket work and look-back once per 4096 elements), denser or
+ * unknown ones two (a four-tile window overflow is correct but slow: the client
+ * goes to the exact path). */
+int fc_quantize_encode_hinted(const float* const* xs, int32_t nclients, int64_t P, float step,
+                              const float* norms, const float* prescale, const int64_t* seeds,
+                              int mode, uint8_t* stream_buf, const int64_t* stream_off,
+                              const int64_t* stream_cap, uint64_t* idx, int64_t* total_bits,
+                              float* dist_part, int32_t* nnz_part, int32_t* overflow,
+                              void* workspace, int64_t workspace_bytes, int64_t max_cap,
+                              void* stream);
+
 /* Segmented quantise + encode (few clients per GPU; same results as
  * fc_quantize_encode, bit for bit).  Each client is cut into nseg element
  * segments (a multiple of 2048 elements each, plus a remainder) encoded as

@@ -46,6 +46,9 @@ if not HAVE:
   sys.exit(0)
 names = ["loop/ticket", "A load+quant+code", "B-D scans+emit", "D tail+reductions", "publish agg",
          "pending lookback+prefix", "pending store"]
+if os.environ.get("ENC2"):  # k_encode2's stamps (intervals ending at each stamp)
+  names = ["scans+emit tile 0", "wait staged tile 1", "quant+code (both tiles)", "scans+emit tile 1",
+           "wait end (next stage, lb window)", "reductions+publish", "look-back", "finish: idx+stores+clear"]
 tot = sum(buf[i] for i in range(len(names)))
 print("encode %.2f ms, %d tiles, %.0f cycles/tile total (memtime units)" % (dt * 1e3, tiles, tot / tiles))
 for i, n in enumerate(names):
