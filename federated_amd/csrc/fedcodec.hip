@@ -846,6 +846,9 @@ __device__ __forceinline__ float div_step(float x, float step, float y) {
   return x / step;
 }
 
+#ifndef FC_NZ_BITS
+#define FC_NZ_BITS 1  // chunk first / last nonzero by bit scans of a nonzero mask (0: select chains)
+#endif
 template <int MODE, int DIV, bool PRE, bool MASK = false, bool PAIR = false>
 __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t g,
                                                      const uint32_t (&r4)[4], int32_t rel0,
@@ -888,9 +891,19 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
   }
   // the chunk's first / last nonzero, as selects here, before the code paths
   // branch (computed after them the compiler turned the chains into branches)
+#if FC_NZ_BITS
+  // from a 4-bit mask of the nonzeros, by bit scans: the select chains below came
+  // out as divergent branches (exec-mask juggling around single adds)
+  uint32_t nzm = (nz[0] ? 1u : 0u) | (nz[1] ? 2u : 0u) | (nz[2] ? 4u : 0u) | (nz[3] ? 8u : 0u);
+  asm volatile("" : "+v"(nzm));
+  int32_t cfirst = nzm ? rel0 + (int32_t)__builtin_ctz(nzm) : -1;
+  int32_t clast = nzm ? rel0 + 31 - (int32_t)__builtin_clz(nzm) : -1;
+  asm volatile("" : "+v"(cfirst), "+v"(clast));
+#else
   int32_t cfirst = nz[0] ? rel0 : (nz[1] ? rel0 + 1 : (nz[2] ? rel0 + 2 : (nz[3] ? rel0 + 3 : -1)));
   int32_t clast = nz[3] ? rel0 + 3 : (nz[2] ? rel0 + 2 : (nz[1] ? rel0 + 1 : (nz[0] ? rel0 : -1)));
   asm volatile("" : "+v"(cfirst), "+v"(clast));
+#endif
   ChunkCode r;
   r.acc = 0;
   r.len = 0;
@@ -2489,6 +2502,12 @@ __device__ __forceinline__ uint32_t lut_entry(uint32_t i) {
 }
 
 constexpr int kDecThreads = 256;
+// Tiles per lane segment (accumulator path), chosen per launch: two with 256
+// lanes per tile pair once there are >= kDecSpan2Clients clients (half the
+// segment starts -- index loads and the first block's round trip -- per code:
+// 1024 x 25 M decode 12.5 -> 11.3 ms); one below (config 2's 128 clients need
+// every segment in flight: 0.45 vs 0.87 ms).
+constexpr int kDecSpan2Clients = 256;
 
 typedef __attribute__((address_space(3))) int32_t* lds_iptr;
 
@@ -2525,7 +2544,7 @@ template <bool PLANE, bool LONG = false, bool STEP3 = false>
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
                                                uint64_t b1, int32_t rel, uint32_t my_addr,
                                                const uint32_t* lut, int32_t* err, int32_t* ptile,
-                                               uint32_t hib) {
+                                               uint32_t hib, uint32_t span = kTE) {
   SegReader r;
   const int32_t total = (int32_t)(b1 - b0);
   r.init(base, cap, b0, total);
@@ -2534,7 +2553,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
   int32_t cons = 0;
   int32_t fill = r.nwin;
   uint32_t relb = my_addr + 4u * (uint32_t)rel;  // byte address of the previous nonzero's slot
-  const uint32_t lo_addr = my_addr, hi_addr = my_addr + 4u * (uint32_t)kTE;
+  const uint32_t lo_addr = my_addr, hi_addr = my_addr + 4u * span;
   uint32_t bad = 0;
   uint32_t it = 0;
   while (cons < total) {
@@ -2637,8 +2656,8 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       // the run may come from far before the tile: bound it before scaling to bytes
       const int32_t rel_now = ((int32_t)(relb - my_addr)) >> 2;
       const uint32_t rel_new = (uint32_t)(rel_now + (int32_t)d);
-      bad |= rel_new >= (uint32_t)kTE ? 1u : 0u;
-      relb = my_addr + 4u * min(rel_new, (uint32_t)kTE - 1);
+      bad |= rel_new >= span ? 1u : 0u;
+      relb = my_addr + 4u * min(rel_new, span - 1);
       acc_add_at<PLANE>(relb, v, ptile, hib);
       cons += (int32_t)L;
     }
@@ -2676,19 +2695,21 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 // clients' values in LDS and writing the tile's sum / dequantised values -- or
 // (PLANE) storing each client's values into its q row (zeroed beforehand), for
 // k_sum_planes to add in client order.
-template <bool PLANE>
+template <bool PLANE, int SPAN_ = 1>
 #ifndef FC_DEC_WPE
 #define FC_DEC_WPE 5  // waves per SIMD the register budget is held to
 #endif
 __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(FC_DEC_WPE))) void k_decode(DecodeArgs a) {
   __shared__ uint32_t lut[kLutSize];  // static: table reads fold its base into the offset
   extern __shared__ int32_t acc[];     // [tiles_per_wg][kTE] sums
+  // a lane's segment: SPAN consecutive tiles of one client (the accumulator path)
+  constexpr int SPAN = PLANE ? 1 : SPAN_;
   const int tid = threadIdx.x;
-  const int tiles_per_wg = kDecThreads / a.lanes_per_tile;
+  const int tiles_per_wg = kDecThreads / a.lanes_per_tile * SPAN;
   for (int i = tid; i < kLutSize; i += kDecThreads) lut[i] = lut_entry((uint32_t)i);
   const int sub = tid / a.lanes_per_tile;
   const int l = tid - sub * a.lanes_per_tile;
-  const uint32_t my_addr = PLANE ? 0u : (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * kTE);
+  const uint32_t my_addr = PLANE ? 0u : (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * SPAN * kTE);
   const int64_t ngroups = (a.t_end - a.t_begin + tiles_per_wg - 1) / tiles_per_wg;
   const int64_t e_end = min(a.P, (int64_t)a.t_end * kTE);  // elements this launch writes
   if (PLANE) __syncthreads();  // the table (the accumulator path's first barrier covers it otherwise)
@@ -2698,9 +2719,11 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(FC_
       for (int i = tid; i < tiles_per_wg * kTE; i += kDecThreads) acc[i] = 0;
       __syncthreads();
     }
-    const int64_t t = t0 + sub;
+    const int64_t t = t0 + sub * SPAN;
     if (t < a.t_end) {
       const int64_t tile_base = t * kTE;
+      const int64_t tE = min<int64_t>(t + SPAN, a.t_end);  // segment end tile
+      const uint32_t span = (uint32_t)(tE - t) * kTE;
       for (int c = l; c < a.nclients; c += a.lanes_per_tile) {
 #if FC_DEC_ABL & 8  // diagnostics: 8 clients' streams and indexes for every lane (cache-resident reads)
         const int cc = c & 7;
@@ -2708,22 +2731,22 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(FC_
         const int cc = c;
 #endif
         const int64_t ib = (int64_t)cc * (a.T + 1) + t;
-        const uint64_t e0 = a.idx[ib], e1 = a.idx[ib + 1];
+        const uint64_t e0 = a.idx[ib], e1 = a.idx[ib + (tE - t)];
+        const int64_t soff = a.stream_off[cc], scap = a.stream_cap[cc];
         const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
         if (bend <= bstart) continue;
         const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
         int32_t* ptile = PLANE ? a.plane + (int64_t)c * a.plane_stride + tile_base : nullptr;
         const uint32_t hib = PLANE ? 4u * (uint32_t)min<int64_t>(kTE, a.P - tile_base) : 0u;
         // a wave whose segments are all long-code streams skips the table steps
-        if (kDecLongBits > 0 && __ballot(bend - bstart < (uint64_t)kDecLongBits * kTE) == 0)
-          decode_segment<PLANE, true>(a.stream_buf + a.stream_off[cc], a.stream_cap[cc], bstart, bend, rel, my_addr,
-                                      lut, a.err, ptile, hib);
-        else if (kDecStep3Bits16 > 0 && __ballot(bend - bstart >= (uint64_t)kDecStep3Bits16 * (kTE / 16)) == 0)
-          decode_segment<PLANE, false, true>(a.stream_buf + a.stream_off[cc], a.stream_cap[cc], bstart, bend, rel,
-                                             my_addr, lut, a.err, ptile, hib);
+        if (kDecLongBits > 0 && __ballot(bend - bstart < (uint64_t)kDecLongBits * span) == 0)
+          decode_segment<PLANE, true>(a.stream_buf + soff, scap, bstart, bend, rel, my_addr, lut, a.err, ptile, hib,
+                                      span);
+        else if (kDecStep3Bits16 > 0 && __ballot(bend - bstart >= (uint64_t)kDecStep3Bits16 * (span / 16)) == 0)
+          decode_segment<PLANE, false, true>(a.stream_buf + soff, scap, bstart, bend, rel, my_addr, lut, a.err, ptile,
+                                             hib, span);
         else
-          decode_segment<PLANE>(a.stream_buf + a.stream_off[cc], a.stream_cap[cc], bstart, bend, rel, my_addr, lut,
-                                a.err, ptile, hib);
+          decode_segment<PLANE>(a.stream_buf + soff, scap, bstart, bend, rel, my_addr, lut, a.err, ptile, hib, span);
       }
     }
     if (PLANE) continue;
@@ -4164,16 +4187,18 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   a.t_end = (int32_t)tile_end;
   // lanes per tile: 128 (two tiles per workgroup; measured 2-3 % faster than 256 at
   // 256 and 1024 clients, 64 is 20 % slower), fewer for few clients
-  int lpt = 128;
+  const bool plane = a.plane != nullptr;
+  int span = (!plane && nclients >= kDecSpan2Clients) ? 2 : 1;
+  if (const char* e = getenv("FEDCODEC_DEC_SPAN")) span = (!plane && atoi(e) == 2) ? 2 : 1;  // test knob
+  int lpt = span == 2 ? 256 : 128;
   while (lpt > 64 && lpt / 2 >= nclients) lpt /= 2;
   if (const char* l = getenv("FEDCODEC_DEC_LPT")) {  // test knob: lanes per tile (64, 128 or 256)
     const int v = atoi(l);
     if (v == 64 || v == 128 || v == 256) lpt = v;
   }
   a.lanes_per_tile = lpt;
-  const bool plane = a.plane != nullptr;
-  void (*kern)(DecodeArgs) = plane ? k_decode<true> : k_decode<false>;
-  const int tpw = kDecThreads / lpt;
+  void (*kern)(DecodeArgs) = plane ? k_decode<true> : span == 2 ? k_decode<false, 2> : k_decode<false, 1>;
+  const int tpw = kDecThreads / lpt * span;
   const size_t lds = plane ? 0 : (size_t)tpw * kTE * sizeof(int32_t);  // + the static kLutSize-word table
   int dev = 0, ncu = 256, per_cu = 0;
   (void)hipGetDevice(&dev);
