@@ -31,6 +31,8 @@ SIGNATURES = {
     "fc_rlgamma_encode": (_INT, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "fc_quantize_encode_hinted": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P,
                                          _P, _P, _P, _P, _I64, _I64, _P]),
+    "fc_quantize_encode_quarters": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P, _P,
+                                           _P, _P, _P, _P, _I64, _P]),
     "fc_segmented_workspace_bytes": (_I64, [_I32, _I64, _I32, _I64]),
     "fc_quantize_encode_segmented": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _I32, _I64, _P, _P, _P, _P,
                                             _P, _P, _P, _P, _P, _I64, _P]),
@@ -39,6 +41,8 @@ SIGNATURES = {
     "fc_decode_accumulate_scaled": (_INT, [_P, _P, _P, _P, _I32, _I64, _P, _P, _P, _P, _P, _I64, _P]),
     "fc_decode_accumulate_tiles": (_INT, [_P, _P, _P, _P, _I32, _I64, _I32, _I32, _P, _P, _P, _F32, _P, _P,
                                           _P]),
+    "fc_decode_accumulate_quarters": (_INT, [_P, _P, _P, _P, _P, _I32, _I64, _I32, _I32, _P, _P, _P, _F32, _P,
+                                             _P, _P]),
     "fc_vote_workspace_bytes": (_I64, [_I32, _I64, _I32]),
     "fc_vote_lengths": (_INT, [_P, _I32, _I64, _P, _I32, _P, _INT, _P, _P, _P, _I64, _P]),
     "fc_dequantize": (_INT, [_P, _I64, _F32, _P, _P, _P]),

@@ -52,6 +52,14 @@ class EncodedBatch:
     self.overflow = torch.zeros(self.nclients, dtype=torch.int32, device=device)
     self.dist_part = torch.empty(self.nclients * self.T, dtype=torch.float32, device=device)
     self.nnz_part = torch.empty(self.nclients * self.T, dtype=torch.int32, device=device)
+    # quarter-tile decoder index (fc_quantize_encode_quarters): valid when `quarters`
+    self.idxq = None
+    self.quarters = False
+
+  def ensure_quarters(self):
+    if self.idxq is None:
+      self.idxq = torch.empty(self.nclients * self.T * 3, dtype=torch.int64, device=self.device)
+    return self.idxq
 
   def bits(self):
     return self.total_bits.cpu().numpy()
@@ -122,6 +130,22 @@ def auto_segments(nclients, P):
   return max(1, min(63, k))
 
 
+def quarter_index_wanted(nclients, nseg=1):
+  """Whether a batch is encoded with the quarter-tile decoder index.
+
+  Few clients (under 256, the decoder's one-tile lane segments) and no
+  segmentation: each lane's serial decode chain bounds the decoder there (config
+  2: 128 clients x 1 M at ~10 bits per element), and four segments per tile and
+  client put four times as many chains in flight.  ``FEDCODEC_QUARTERS`` (0 / 1)
+  overrides.
+  """
+  import os  # pylint: disable=g-import-not-at-top
+  env = os.environ.get("FEDCODEC_QUARTERS")
+  if env:
+    return env != "0" and int(nseg) <= 1
+  return int(nseg) <= 1 and int(nclients) < 256
+
+
 def _ptr_array(tensors, device):
   return torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64, device=device)
 
@@ -142,14 +166,16 @@ def _rows(xs, dtype):
 
 
 def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, ptrs=None,
-                    out=None, P=None, prescale=None, segments=None):
+                    out=None, P=None, prescale=None, segments=None, quarters=None):
   """fc_quantize_encode over a batch.  ``xs``: [C, P] tensor or list of tensors.
 
   ``seeds``: int64 tensor [C, 2] (device or host).  ``norms``: optional device
   float32 [C] (client step = norms[c] * step).  Returns an EncodedBatch.
   ``ptrs``/``P``/``out`` let hot loops reuse a pointer array and buffers.
   ``segments``: segments per client for fc_quantize_encode_segmented (same
-  output bit for bit; None: ``auto_segments``, 1: off).
+  output bit for bit; None: ``auto_segments``, 1: off).  ``quarters``: also
+  build the quarter-tile decoder index (fc_quantize_encode_quarters; None:
+  ``quarter_index_wanted``; never with segments).
   """
   _lib.require_gpu()
   if ptrs is None:
@@ -173,14 +199,24 @@ def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, p
                 _lib.ptr(out.stream_off), _lib.ptr(out.stream_cap), _lib.ptr(out.idx), _lib.ptr(out.total_bits),
                 _lib.ptr(out.dist_part), _lib.ptr(out.nnz_part), _lib.ptr(out.overflow), _lib.ptr(sws),
                 sws.numel(), _lib.stream_handle(stream))
+      out.quarters = False
       return out
   ws = _WS.get(C, P, device)
+  if quarter_index_wanted(C, nseg) if quarters is None else quarters:
+    _lib.call("fc_quantize_encode_quarters", _lib.ptr(ptrs), C, P, float(step), _lib.ptr(norms),
+              _lib.ptr(prescale), _lib.ptr(seeds), int(mode), _lib.ptr(out.stream), _lib.ptr(out.stream_off),
+              _lib.ptr(out.stream_cap), _lib.ptr(out.idx), _lib.ptr(out.ensure_quarters()),
+              _lib.ptr(out.total_bits), _lib.ptr(out.dist_part), _lib.ptr(out.nnz_part), _lib.ptr(out.overflow),
+              _lib.ptr(ws), ws.numel(), _lib.stream_handle(stream))
+    out.quarters = True
+    return out
   # the largest capacity hints the expected code density (fc_quantize_encode_hinted)
   _lib.call("fc_quantize_encode_hinted", _lib.ptr(ptrs), C, P, float(step), _lib.ptr(norms),
             _lib.ptr(prescale), _lib.ptr(seeds), int(mode), _lib.ptr(out.stream), _lib.ptr(out.stream_off),
             _lib.ptr(out.stream_cap), _lib.ptr(out.idx), _lib.ptr(out.total_bits),
             _lib.ptr(out.dist_part), _lib.ptr(out.nnz_part), _lib.ptr(out.overflow),
             _lib.ptr(ws), ws.numel(), int(out.caps_host.max()), _lib.stream_handle(stream))
+  out.quarters = False
   return out
 
 
@@ -207,7 +243,7 @@ def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None, presca
   sel = torch.as_tensor(bad, dtype=torch.int64, device=device)
   seeds = torch.as_tensor(seeds, dtype=torch.int64).reshape(C, 2).to(device)
   need = (batch.bits()[bad] + 7) // 8 + 256
-  sub = quantize_encode([rows[c] for c in bad], step, seeds[sel], mode, segments=1,
+  sub = quantize_encode([rows[c] for c in bad], step, seeds[sel], mode, segments=1, quarters=batch.quarters,
                         norms=None if norms is None else norms[sel], caps=list(need),
                         prescale=None if prescale is None else
                         torch.as_tensor(prescale).reshape(C, 2).to(device)[sel].contiguous())
@@ -234,6 +270,10 @@ def _repack(batch, sub, bad, caps):
     dst, src, rep = getattr(out, name), getattr(batch, name), getattr(sub, name)
     dst.copy_(src)
     dst.view(C, width).index_copy_(0, sel, rep.view(len(bad), width))
+  if batch.quarters:
+    out.ensure_quarters().copy_(batch.idxq)
+    out.idxq.view(C, 3 * T).index_copy_(0, sel, sub.idxq.view(len(bad), 3 * T))
+    out.quarters = True
   nbytes = batch.nbytes()
   sub_nbytes = sub.nbytes()
   is_bad = np.zeros(C, bool)
@@ -312,6 +352,18 @@ def decode_accumulate(batch, sum_in=None, want_sum=True, out=None, step=1.0, noi
   device = batch.device
   if want_sum and sum_out is None:
     sum_out = torch.empty(batch.P, dtype=torch.int32, device=device)
+  if batch.quarters:  # quarter-tile lane segments (fc_decode_accumulate_quarters ORs into err)
+    if err is None:
+      err = torch.zeros(1, dtype=torch.int32, device=device)
+    elif tiles is None:
+      with torch.cuda.stream(stream):
+        err.zero_()
+    t0, t1 = (0, batch.T) if tiles is None else tiles
+    _lib.call("fc_decode_accumulate_quarters", _lib.ptr(batch.stream), _lib.ptr(batch.stream_off),
+              _lib.ptr(batch.stream_cap), _lib.ptr(batch.idx), _lib.ptr(batch.idxq), batch.nclients, batch.P,
+              int(t0), int(t1), _lib.ptr(sum_in), _lib.ptr(sum_out if want_sum else None), _lib.ptr(out),
+              float(step), _lib.ptr(noise_sum), _lib.ptr(err), _lib.stream_handle(stream))
+    return (sum_out if want_sum else None), out, err
   if err is None:
     err = torch.zeros(1, dtype=torch.int32, device=device)
   if tiles is None:

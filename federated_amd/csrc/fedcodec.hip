@@ -281,7 +281,19 @@ struct EncodeArgs {
   int32_t T2;             // super-tiles (two tiles) per client: k_encode2's tickets and statuses
   const int64_t* elem_off;  // nullable [C]: element offset (multiple of 4) of row c in its client's
                             // tensor -- the row is a segment; its Philox stream continues there
+  uint64_t* idxq;           // nullable [C * T][3]: quarter-tile decoder entries (k_encode and the
+                            // exact path write them tile-relative, k_quarter_index rebases them)
 };
+
+// Quarter-tile entries (elements 256 s of a tile, s = 1..3), tile-relative as the
+// encoder writes them: [0, 24) body bits before the quarter's first code (after the
+// tile's leading run code), [24, 35) 1 + the tile's last nonzero before the quarter
+// (0: none), [35, 46) 1 + the tile's first nonzero.  k_quarter_index turns them into
+// decoder entries (absolute bit offset | 1 + last nonzero before << 36).
+__device__ __forceinline__ uint64_t quarter_rel(uint32_t off, int32_t prev, int32_t first) {
+  return (uint64_t)(off & 0xFFFFFFu) | ((uint64_t)(uint32_t)(prev + 1) << 24) |
+         ((uint64_t)(uint32_t)(first + 1) << 35);
+}
 
 // The launch's EncodeArgs re-read from the kernarg segment (k_encode and
 // k_encode_exact take EncodeArgs as their only argument, at offset 0).  The
@@ -1570,6 +1582,23 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
       const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;
       const uint64_t fm = __ballot(lfirst >= 0);  // lanes are in element order
       const int32_t tile_first = fm ? __builtin_amdgcn_readlane(lfirst, (int)__builtin_ctzll(fm)) : -1;
+      if (uint64_t* const iq = enc_args_fresh().idxq) {
+        // quarter starts (lanes 16, 32, 48): the body offset of the lane's first code
+        // and the last nonzero before it (a slow tile's client is redone by the exact path)
+        const uint32_t xo = is - ltot;
+        const uint64_t q1 = quarter_rel(__builtin_amdgcn_readlane(xo, 16), __builtin_amdgcn_readlane(lprev, 16),
+                                        tile_first);
+        const uint64_t q2 = quarter_rel(__builtin_amdgcn_readlane(xo, 32), __builtin_amdgcn_readlane(lprev, 32),
+                                        tile_first);
+        const uint64_t q3 = quarter_rel(__builtin_amdgcn_readlane(xo, 48), __builtin_amdgcn_readlane(lprev, 48),
+                                        tile_first);
+        if (lane == 0) {
+          uint64_t* q = iq + 3 * ((int64_t)c * a.T + t);
+          q[0] = q1;
+          q[1] = q2;
+          q[2] = q3;
+        }
+      }
       if (fast && !(FC_ABL & 32)) {
         const float d = DIV == 1 ? dsum * (cp.step * cp.step) : dsum;  // DIV 1: sums of (sc - r)^2
         const int32_t n = INT_IN ? wave_sum_i(nnz) : nnz;
@@ -2165,6 +2194,13 @@ __global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
     const int32_t tile_last = sc.carry;
     const int32_t tile_first = wave_min_i(sc.wfirst);
     const uint32_t body = sc.body;
+    if (a.idxq && lane == 0) {  // quarter j = chunk j: lane 0 holds its offset and predecessor
+      uint64_t* q = a.idxq + 3 * ((int64_t)c * a.T + t);
+      const int32_t f = tile_last >= 0 ? tile_first : -1;
+      q[0] = quarter_rel(sc.chunk_off[1], sc.chunk_prev[1], f);
+      q[1] = quarter_rel(sc.chunk_off[2], sc.chunk_prev[2], f);
+      q[2] = quarter_rel(sc.chunk_off[3], sc.chunk_prev[3], f);
+    }
     {
       const float d = wave_sum_f(sc.dist);
       const int32_t nz = wave_sum_i(sc.nnz);
@@ -2254,6 +2290,7 @@ struct DecodeArgs {
   int32_t* plane;             // PLANE: q of each client, row c at plane + c * plane_stride
   int64_t plane_stride;
   int32_t t_begin, t_end;     // tiles decoded: [t_begin, t_end)
+  const uint64_t* idxq;       // nullable [nclients * T][3]: quarter-tile entries (lane segments of 256)
 };
 
 // General decode of one code at absolute bit position pos straight from
@@ -2694,36 +2731,48 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 // (tiles_per_wg at a time) with one lane per client segment, accumulating the
 // clients' values in LDS and writing the tile's sum / dequantised values -- or
 // (PLANE) storing each client's values into its q row (zeroed beforehand), for
-// k_sum_planes to add in client order.
-template <bool PLANE, int SPAN_ = 1>
+// k_sum_planes to add in client order.  QTR: the lane segments are quarter tiles
+// (256 elements, entries from the quarter index): four times the segments in
+// flight for few clients with dense codes (config 2: 128 clients, ~10 bits per
+// element -- each lane's serial chain, not memory, bounds the decode).
+template <bool PLANE, int SPAN_ = 1, bool QTR = false>
 #ifndef FC_DEC_WPE
 #define FC_DEC_WPE 5  // waves per SIMD the register budget is held to
 #endif
-__global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(FC_DEC_WPE))) void k_decode(DecodeArgs a) {
+#ifndef FC_DEC_QTR_WPE
+#define FC_DEC_QTR_WPE 5  // the same for quarter-tile segments (measured: 5 and 6 even, 8 spills: +12 %)
+#endif
+__global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR ? FC_DEC_QTR_WPE : FC_DEC_WPE))) void k_decode(DecodeArgs a) {
   __shared__ uint32_t lut[kLutSize];  // static: table reads fold its base into the offset
-  extern __shared__ int32_t acc[];     // [tiles_per_wg][kTE] sums
-  // a lane's segment: SPAN consecutive tiles of one client (the accumulator path)
+  extern __shared__ int32_t acc[];     // [units_per_wg][UE] sums
+  // a lane's segment: SPAN consecutive units of one client (the accumulator path)
   constexpr int SPAN = PLANE ? 1 : SPAN_;
+  constexpr int UE = QTR ? kTE / 4 : kTE;  // elements per unit (tile or quarter tile)
+  constexpr int UPT = kTE / UE;            // units per tile
   const int tid = threadIdx.x;
-  const int tiles_per_wg = kDecThreads / a.lanes_per_tile * SPAN;
+  const int units_per_wg = kDecThreads / a.lanes_per_tile * SPAN;
   for (int i = tid; i < kLutSize; i += kDecThreads) lut[i] = lut_entry((uint32_t)i);
   const int sub = tid / a.lanes_per_tile;
   const int l = tid - sub * a.lanes_per_tile;
-  const uint32_t my_addr = PLANE ? 0u : (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * SPAN * kTE);
-  const int64_t ngroups = (a.t_end - a.t_begin + tiles_per_wg - 1) / tiles_per_wg;
+  const uint32_t my_addr = PLANE ? 0u : (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * SPAN * UE);
   const int64_t e_end = min(a.P, (int64_t)a.t_end * kTE);  // elements this launch writes
+  const int64_t u_begin = (int64_t)a.t_begin * UPT;
+  const int64_t u_end = (e_end + UE - 1) / UE;  // units holding elements of the range
+  const int64_t ngroups = (u_end - u_begin + units_per_wg - 1) / units_per_wg;
   if (PLANE) __syncthreads();  // the table (the accumulator path's first barrier covers it otherwise)
   for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const int64_t t0 = a.t_begin + grp * tiles_per_wg;
+    const int64_t u0 = u_begin + grp * units_per_wg;
     if (!PLANE) {
-      for (int i = tid; i < tiles_per_wg * kTE; i += kDecThreads) acc[i] = 0;
+      for (int i = tid; i < units_per_wg * UE; i += kDecThreads) acc[i] = 0;
       __syncthreads();
     }
-    const int64_t t = t0 + sub * SPAN;
-    if (t < a.t_end) {
-      const int64_t tile_base = t * kTE;
-      const int64_t tE = min<int64_t>(t + SPAN, a.t_end);  // segment end tile
-      const uint32_t span = (uint32_t)(tE - t) * kTE;
+    const int64_t u = u0 + sub * SPAN;
+    if (u < u_end) {
+      const int64_t unit_base = u * UE;
+      const int64_t uE = min<int64_t>(u + SPAN, u_end);  // segment end unit
+      const uint32_t span = (uint32_t)(uE - u) * UE;
+      const int64_t t = u / UPT;
+      const int qs = (int)(u - t * UPT);  // QTR: quarter of the tile
       for (int c = l; c < a.nclients; c += a.lanes_per_tile) {
 #if FC_DEC_ABL & 8  // diagnostics: 8 clients' streams and indexes for every lane (cache-resident reads)
         const int cc = c & 7;
@@ -2731,13 +2780,21 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(FC_
         const int cc = c;
 #endif
         const int64_t ib = (int64_t)cc * (a.T + 1) + t;
-        const uint64_t e0 = a.idx[ib], e1 = a.idx[ib + (tE - t)];
+        uint64_t e0, e1;
+        if (QTR) {
+          const uint64_t* q = a.idxq + 3 * ((int64_t)cc * a.T + t);
+          e0 = qs == 0 ? a.idx[ib] : q[qs - 1];
+          e1 = qs == 3 ? a.idx[ib + 1] : q[qs];
+        } else {
+          e0 = a.idx[ib];
+          e1 = a.idx[ib + (uE - u)];
+        }
         const int64_t soff = a.stream_off[cc], scap = a.stream_cap[cc];
         const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
         if (bend <= bstart) continue;
-        const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - tile_base);  // last nonzero, tile-relative
-        int32_t* ptile = PLANE ? a.plane + (int64_t)c * a.plane_stride + tile_base : nullptr;
-        const uint32_t hib = PLANE ? 4u * (uint32_t)min<int64_t>(kTE, a.P - tile_base) : 0u;
+        const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - unit_base);  // last nonzero, unit-relative
+        int32_t* ptile = PLANE ? a.plane + (int64_t)c * a.plane_stride + unit_base : nullptr;
+        const uint32_t hib = PLANE ? 4u * (uint32_t)min<int64_t>(kTE, a.P - unit_base) : 0u;
         // a wave whose segments are all long-code streams skips the table steps
         if (kDecLongBits > 0 && __ballot(bend - bstart < (uint64_t)kDecLongBits * span) == 0)
           decode_segment<PLANE, true>(a.stream_buf + soff, scap, bstart, bend, rel, my_addr, lut, a.err, ptile, hib,
@@ -2751,8 +2808,8 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(FC_
     }
     if (PLANE) continue;
     __syncthreads();
-    for (int i = tid; i < tiles_per_wg * kTE; i += kDecThreads) {
-      const int64_t e = t0 * kTE + i;
+    for (int i = tid; i < units_per_wg * UE; i += kDecThreads) {
+      const int64_t e = u0 * UE + i;
       if (e >= e_end) break;
       int32_t v = acc[i];
       if (a.sum_in) v = (int32_t)((uint32_t)v + (uint32_t)a.sum_in[e]);
@@ -3548,12 +3605,38 @@ int64_t enc_workspace_bytes(int32_t n, int64_t P) {
   return enc_params_offset(n, P) + (int64_t)n * (int64_t)sizeof(ClientParam);
 }
 
+// Quarter-tile decoder entries: the encoder's tile-relative records (quarter_rel)
+// rebased on the tile's own entry -- the stream bit where the tile's codes start and
+// its predecessor nonzero -- after the tile's leading run code.  A quarter with no
+// nonzero of the tile before it starts where the tile does.
+__global__ void k_quarter_index(const uint64_t* __restrict__ idx, uint64_t* __restrict__ idxq, int32_t nclients,
+                                int32_t T) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // c * T + t
+  if (i >= (int64_t)nclients * T) return;
+  const int64_t c = i / T, t = i - c * T;
+  const uint64_t e = idx[c * (T + 1) + t];
+  const uint64_t body = e & kMask36;
+  const int64_t last = (int64_t)(e >> 36) - 1;
+  const int64_t tile_base = t * kTE;
+  for (int s = 0; s < 3; ++s) {
+    const uint64_t r = idxq[3 * i + s];
+    const int32_t prev = (int32_t)((r >> 24) & 0x7FFu) - 1;
+    const int32_t first = (int32_t)((r >> 35) & 0x7FFu) - 1;
+    uint64_t o = e;
+    if (prev >= 0) {
+      const uint32_t R0 = glen((uint32_t)(tile_base + first - last));
+      o = ((body + R0 + (r & 0xFFFFFFu)) & kMask36) | ((uint64_t)(tile_base + prev + 1) << 36);
+    }
+    idxq[3 * i + s] = o;
+  }
+}
+
 int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step, const float* norms,
                   const float* prescale, const int64_t* seeds, int mode, bool int_in, uint8_t* stream_buf,
                   const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
                   int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow,
                   void* workspace, int64_t workspace_bytes, void* stream, const int64_t* elem_off = nullptr,
-                  int64_t max_cap = 0) {
+                  int64_t max_cap = 0, uint64_t* idxq = nullptr) {
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
   if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
   if (!xs || !stream_buf || !stream_off || !stream_cap || !idx || !total_bits || !overflow)
@@ -3571,6 +3654,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   if (hipMemsetAsync(overflow, 0, sizeof(int32_t) * nclients, s) != hipSuccess) return fail(-10, "memset overflow");
   EncodeArgs a;
   a.elem_off = elem_off;
+  a.idxq = idxq;
   a.xs = xs;
   a.nclients = nclients;
   a.P = P;
@@ -3650,6 +3734,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
     per_cu0 = 1;
   bool super = (int64_t)ncu * per_cu0 * kEnc2Waves <= 4LL * nclients && T >= 2;
   if (const char* e = getenv("FEDCODEC_ENC2")) super = atoi(e) != 0;  // test knob
+  if (idxq) super = false;  // quarter-tile entries come from the one-tile kernel (few clients)
   // four tiles per ticket (FEDCODEC_ENC_NT=4): the per-ticket work (ticket, status,
   // look-back, reductions, store set-up) paid once per 4096 elements; the window
   // (the same LDS) then holds about 8.4 bits per element before the exact path
@@ -3689,6 +3774,12 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   // clients with a tile beyond the fast path: exact re-encode (no-ops otherwise)
   hipLaunchKernelGGL(k_zero_slow, dim3(256), dim3(256), 0, s, a);
   hipLaunchKernelGGL(exact, dim3(grid), dim3(kEncThreads), 0, s, a);
+  if (idxq) {
+    if (hipGetLastError() != hipSuccess) return check_launch("k_encode_exact");
+    hipLaunchKernelGGL(k_quarter_index, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, idx, idxq,
+                       nclients, (int32_t)T);
+    return check_launch("k_quarter_index");
+  }
   return check_launch("k_encode_exact");
 }
 
@@ -4188,8 +4279,9 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   // lanes per tile: 128 (two tiles per workgroup; measured 2-3 % faster than 256 at
   // 256 and 1024 clients, 64 is 20 % slower), fewer for few clients
   const bool plane = a.plane != nullptr;
-  int span = (!plane && nclients >= kDecSpan2Clients) ? 2 : 1;
-  if (const char* e = getenv("FEDCODEC_DEC_SPAN")) span = (!plane && atoi(e) == 2) ? 2 : 1;  // test knob
+  const bool qtr = !plane && a.idxq != nullptr;  // quarter-tile lane segments
+  int span = (!plane && !qtr && nclients >= kDecSpan2Clients) ? 2 : 1;
+  if (const char* e = getenv("FEDCODEC_DEC_SPAN")) span = (!plane && !qtr && atoi(e) == 2) ? 2 : 1;  // test knob
   int lpt = span == 2 ? 256 : 128;
   while (lpt > 64 && lpt / 2 >= nclients) lpt /= 2;
   if (const char* l = getenv("FEDCODEC_DEC_LPT")) {  // test knob: lanes per tile (64, 128 or 256)
@@ -4197,17 +4289,22 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
     if (v == 64 || v == 128 || v == 256) lpt = v;
   }
   a.lanes_per_tile = lpt;
-  void (*kern)(DecodeArgs) = plane ? k_decode<true> : span == 2 ? k_decode<false, 2> : k_decode<false, 1>;
-  const int tpw = kDecThreads / lpt * span;
-  const size_t lds = plane ? 0 : (size_t)tpw * kTE * sizeof(int32_t);  // + the static kLutSize-word table
+  void (*kern)(DecodeArgs) = plane ? k_decode<true>
+                             : qtr     ? k_decode<false, 1, true>
+                             : span == 2 ? k_decode<false, 2> : k_decode<false, 1>;
+  const int ue = qtr ? kTE / 4 : kTE;  // elements per unit
+  const int tpw = kDecThreads / lpt * span;  // units per workgroup
+  const size_t lds = plane ? 0 : (size_t)tpw * ue * sizeof(int32_t);  // + the static kLutSize-word table
   int dev = 0, ncu = 256, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kDecThreads, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
-  const int64_t ngroups = (a.t_end - a.t_begin + tpw - 1) / tpw;
+  const int64_t u_end = (std::min<int64_t>(P, (int64_t)a.t_end * kTE) + ue - 1) / ue;
+  const int64_t ngroups = (u_end - (int64_t)a.t_begin * (kTE / ue) + tpw - 1) / tpw;
   // 5 workgroups/CU: more waves only add L2 line thrash (measured 4.2 ms at 5/CU vs 5.0 at 7/CU)
-  int64_t max_grid = (int64_t)ncu * std::min(per_cu, 5);
+  // (quarter-tile segments: every co-resident workgroup -- short chains, few lines each)
+  int64_t max_grid = (int64_t)ncu * std::min(per_cu, qtr ? 8 : 5);
   if (const char* g = getenv("FEDCODEC_DEC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
   const dim3 grid((unsigned)std::min<int64_t>(ngroups, max_grid));
   hipStream_t s = (hipStream_t)stream;
@@ -4293,6 +4390,18 @@ int fc_quantize_encode_hinted(const float* const* xs, int32_t nclients, int64_t 
                        workspace_bytes, stream, nullptr, max_cap);
 }
 
+int fc_quantize_encode_quarters(const float* const* xs, int32_t nclients, int64_t P, float step,
+                                const float* norms, const float* prescale, const int64_t* seeds, int mode,
+                                uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap,
+                                uint64_t* idx, uint64_t* idxq, int64_t* total_bits, float* dist_part,
+                                int32_t* nnz_part, int32_t* overflow, void* workspace, int64_t workspace_bytes,
+                                void* stream) {
+  if (!idxq) return fail(-1, "null required pointer");
+  return encode_common((const void* const*)xs, nclients, P, step, norms, prescale, seeds, mode, false, stream_buf,
+                       stream_off, stream_cap, idx, total_bits, dist_part, nnz_part, overflow, workspace,
+                       workspace_bytes, stream, nullptr, 0, idxq);
+}
+
 int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P, uint8_t* stream_buf,
                       const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
                       int64_t* total_bits, int32_t* overflow, void* workspace, int64_t workspace_bytes,
@@ -4327,6 +4436,24 @@ int fc_decode_accumulate_tiles(const uint8_t* stream_buf, const int64_t* stream_
   a.out = out;
   a.step = step;
   a.noise_sum = noise_sum;
+  return decode_common(a, stream_buf, stream_off, stream_cap, idx, nclients, P, err, stream, tile_begin,
+                       tile_end, false);
+}
+
+int fc_decode_accumulate_quarters(const uint8_t* stream_buf, const int64_t* stream_off,
+                                  const int64_t* stream_cap, const uint64_t* idx, const uint64_t* idxq,
+                                  int32_t nclients, int64_t P, int32_t tile_begin, int32_t tile_end,
+                                  const int32_t* sum_in, int32_t* sum_out, float* out, float step,
+                                  const float* noise_sum, int32_t* err, void* stream) {
+  if (!sum_out && !out) return fail(-1, "one of sum_out / out required");
+  if (!idxq) return fail(-1, "null required pointer");
+  DecodeArgs a{};
+  a.sum_in = sum_in;
+  a.sum_out = sum_out;
+  a.out = out;
+  a.step = step;
+  a.noise_sum = noise_sum;
+  a.idxq = idxq;
   return decode_common(a, stream_buf, stream_off, stream_cap, idx, nclients, P, err, stream, tile_begin,
                        tile_end, false);
 }

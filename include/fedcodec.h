@@ -147,6 +147,22 @@ int fc_quantize_encode_segmented(const float* const* xs, int32_t nclients, int64
                                  int32_t* overflow, void* workspace, int64_t workspace_bytes,
                                  void* stream);
 
+/* fc_quantize_encode plus a quarter-tile decoder index: idxq = device
+ * uint64[nclients * fc_num_tiles(P) * 3], entry 3 (c * tiles + t) + s - 1 = the
+ * decoder entry (bit offset | 1 + last nonzero before, << 36) of elements
+ * [1024 t + 256 s, ...) for s = 1..3.  Same codes, index and measurements bit for
+ * bit; the extra entries let fc_decode_accumulate_quarters run four lane segments
+ * per tile and client (few clients with dense codes: each segment's serial decode
+ * chain, not memory, bounds the decoder).  Replaces the same reference call as
+ * fc_quantize_encode (quantize_encode.py:139-156 + elias_gamma_encode.py:97-99). */
+int fc_quantize_encode_quarters(const float* const* xs, int32_t nclients, int64_t P, float step,
+                                const float* norms, const float* prescale, const int64_t* seeds,
+                                int mode, uint8_t* stream_buf, const int64_t* stream_off,
+                                const int64_t* stream_cap, uint64_t* idx, uint64_t* idxq,
+                                int64_t* total_bits, float* dist_part, int32_t* nnz_part,
+                                int32_t* overflow, void* workspace, int64_t workspace_bytes,
+                                void* stream);
+
 /* tfc.run_length_gamma_encode over int32 inputs (same batch layout as above,
  * qs = device array of device pointers to int32[P]). */
 int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P,
@@ -176,6 +192,17 @@ int fc_decode_accumulate_tiles(const uint8_t* stream_buf, const int64_t* stream_
                                int64_t P, int32_t tile_begin, int32_t tile_end,
                                const int32_t* sum_in, int32_t* sum_out, float* out, float step,
                                const float* noise_sum, int32_t* err, void* stream);
+
+/* fc_decode_accumulate_tiles over a batch encoded with fc_quantize_encode_quarters:
+ * lane segments of 256 elements (entries from idxq).  Same results bit for bit;
+ * err is OR'ed into, not cleared.  Replaces elias_gamma_encode.py:118-120's decode
+ * + the int32 sum (quantize_encode.py:169-171) like fc_decode_accumulate. */
+int fc_decode_accumulate_quarters(const uint8_t* stream_buf, const int64_t* stream_off,
+                                  const int64_t* stream_cap, const uint64_t* idx,
+                                  const uint64_t* idxq, int32_t nclients, int64_t P,
+                                  int32_t tile_begin, int32_t tile_end, const int32_t* sum_in,
+                                  int32_t* sum_out, float* out, float step, const float* noise_sum,
+                                  int32_t* err, void* stream);
 
 /* QSGD server side (qsgd.py:85-112 sum_encoded_value): acc = fsum_in[i] (or 0),
  * then acc = acc + float(q_c[i]) * client_scale[c] for c = 0 .. nclients-1 in
