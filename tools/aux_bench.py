@@ -46,3 +46,16 @@ timed("dequantize (2^25)", lambda: codec.dequantize(big.view(torch.int32), 0.5),
 del big
 H = [torch.randn(1 << 24, generator=g, device=dev) for _ in range(64)]
 timed("hadamard 64 x 2^24 (fwd)", lambda: codec.hadamard_(H, (1, 2)), 64 * (1 << 24) * 4 * 2)
+del H
+# QSGD server sum (qsgd.py:85-112): the clients' q rows decoded into int32 planes (groups of <= 1 GiB), then
+# k_sum_planes adds float(q_c) * step_c in client order.  Traffic: code read + 4P write + 4P read per client.
+ns = codec.client_norms(rows, _lib.NORM_L2)
+steps = (ns / 16.0).contiguous()  # num_steps 16
+qb = codec.quantize_encode_checked(rows, 1.0, seeds, _lib.STOCHASTIC, norms=steps)
+code_bytes = int(qb.nbytes().sum())
+ws = torch.empty(int(_lib.load().fc_decode_scaled_workspace_bytes(C, P)), dtype=torch.uint8, device=dev)
+qout = torch.empty(P, dtype=torch.float32, device=dev)
+timed("qsgd decode+ordered sum (C x 25M)", lambda: codec.decode_accumulate_scaled(qb, steps, out=qout, workspace=ws),
+      code_bytes + C * P * 8)
+timed("int32 sum decode, same codes", lambda: codec.decode_accumulate(qb, want_sum=False, out=qout, step=1.0),
+      code_bytes + P * 4)
