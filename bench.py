@@ -277,11 +277,14 @@ def codec_round(name, rows, ptrs, P, step, mode, steps, warmup, stream, workload
                                                       stream=stream))
     t.phase("k_decode", lambda: codec.decode_accumulate(batch, want_sum=False, out=out, step=step, err=err,
                                                         stream=stream))
+    # a segmented batch's stitch runs on a second stream beside the decode: the
+    # round ends when it has (the wait's phase is the stitch's time past the decode)
+    t.phase("stitch_join", lambda: batch.join(stream))
   ms = tm.ms()
   if len(codec.check_overflow(batch)) or int(err.item()):
     raise SystemExit("%s: overflow or malformed stream" % name)
   S = float(batch.nbytes().astype(np.float64).sum())
-  t_step = ms["k_encode"] + ms["k_decode"]
+  t_step = ms["k_encode"] + ms["k_decode"] + ms["stitch_join"]
   return {
       "workload": name, "clients": C, "P": P, "mode": [k for k, v in MODES.items() if v == mode][0],
       "step_size": step, "ms_per_step": round(t_step, 3),
@@ -578,6 +581,7 @@ def main():
         w.wait()
       _lib.call("fc_dequantize", _lib.ptr(isum), P, float(args.step_size), None, _lib.ptr(out),
                 _lib.stream_handle(stream))
+    batch.join(stream)  # a segmented batch's stitch (second stream) is part of the round
 
   for _ in range(args.warmup):
     step()
@@ -621,6 +625,7 @@ def main():
                                                        out=batch, stream=stream))
     tm.phase("k_decode", lambda: codec.decode_accumulate(batch, want_sum=False, out=out, step=args.step_size,
                                                          err=err, stream=stream))
+    batch.join(stream)
   ms = tm.ms()
   enc_bytes = Cg * 4.0 * P + S  # fp32 read + code write
   dec_bytes = S + 4.0 * P  # code read + f32 result write

@@ -34,6 +34,10 @@ SIGNATURES = {
     "fc_quantize_encode_quarters": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P, _P,
                                            _P, _P, _P, _P, _I64, _P]),
     "fc_segmented_workspace_bytes": (_I64, [_I32, _I64, _I32, _I64]),
+    "fc_quantize_encode_segmented_split": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _I32, _I64, _P, _P, _P,
+                                                  _P, _P, _P, _P, _P, _P, _I64, _P, _P]),
+    "fc_decode_accumulate_segmented": (_INT, [_P, _I64, _I32, _I64, _I32, _I64, _I32, _I32, _P, _P, _P, _F32, _P,
+                                              _P, _P]),
     "fc_quantize_encode_segmented": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _I32, _I64, _P, _P, _P, _P,
                                             _P, _P, _P, _P, _P, _I64, _P]),
     "fc_decode_accumulate": (_INT, [_P, _P, _P, _P, _I32, _I64, _P, _P, _P, _F32, _P, _P, _P]),

@@ -44,17 +44,61 @@ class EncodedBatch:
     offs[1:] = np.cumsum(caps)[:-1]
     self.caps_host = np.asarray(caps, np.int64)
     self.offs_host = offs
-    self.stream = torch.empty(int(sum(caps)) + _ALIGN, dtype=torch.uint8, device=device)
+    self._stream = torch.empty(int(sum(caps)) + _ALIGN, dtype=torch.uint8, device=device)
     self.stream_off = torch.from_numpy(offs).to(device)
     self.stream_cap = torch.from_numpy(self.caps_host).to(device)
-    self.idx = torch.empty(self.nclients * (self.T + 1), dtype=torch.int64, device=device)
+    self._idx = torch.empty(self.nclients * (self.T + 1), dtype=torch.int64, device=device)
     self.total_bits = torch.empty(self.nclients, dtype=torch.int64, device=device)
     self.overflow = torch.zeros(self.nclients, dtype=torch.int32, device=device)
-    self.dist_part = torch.empty(self.nclients * self.T, dtype=torch.float32, device=device)
-    self.nnz_part = torch.empty(self.nclients * self.T, dtype=torch.int32, device=device)
+    self._dist_part = torch.empty(self.nclients * self.T, dtype=torch.float32, device=device)
+    self._nnz_part = torch.empty(self.nclients * self.T, dtype=torch.int32, device=device)
     # quarter-tile decoder index (fc_quantize_encode_quarters): valid when `quarters`
     self.idxq = None
     self.quarters = False
+    # segmented encode with the stitch on a second stream: `seg` = (workspace, segments,
+    # max_cap) of the unstitched segments (decodable at once), `_pending` = the stitch's
+    # completion event; the code bytes, index and partials are read after a join
+    self.seg = None
+    self._seg_ws = None
+    self._pending = None
+
+  def join(self, stream=None):
+    """Order `stream` (default: the current one) after a pending stitch."""
+    if self._pending is not None:
+      (stream if stream is not None else torch.cuda.current_stream()).wait_event(self._pending)
+      self._pending = None
+
+  def seg_workspace(self, nseg, max_cap):
+    """This batch's own segmented-encode workspace (256-byte aligned; the unstitched
+    segments stay in it for the decode), or None if segmentation is impossible."""
+    need = int(_lib.load().fc_segmented_workspace_bytes(self.nclients, self.P, int(nseg), int(max_cap)))
+    if need < 0:
+      return None
+    if self._seg_ws is None or self._seg_ws.numel() < need + 256:
+      self._seg_ws = None
+      self._seg_ws = torch.empty(_round_up(need + 256, 256), dtype=torch.uint8, device=self.device)
+    off = (-self._seg_ws.data_ptr()) % 256
+    return self._seg_ws[off:off + need]
+
+  @property
+  def stream(self):
+    self.join()
+    return self._stream
+
+  @property
+  def idx(self):
+    self.join()
+    return self._idx
+
+  @property
+  def dist_part(self):
+    self.join()
+    return self._dist_part
+
+  @property
+  def nnz_part(self):
+    self.join()
+    return self._nnz_part
 
   def ensure_quarters(self):
     if self.idxq is None:
@@ -72,6 +116,26 @@ class EncodedBatch:
     nb = int((int(self.total_bits[c].item()) + 7) // 8)
     off = int(self.offs_host[c])
     return bytes(self.stream[off:off + nb].cpu().numpy().tobytes())
+
+
+def split_stitch_wanted():
+  """Whether a segmented batch stitches on a second stream while the round decodes
+  the unstitched segments (fc_decode_accumulate_segmented).  Off by default
+  (``FEDCODEC_SPLIT_STITCH=1`` turns it on): the concurrent copy slows the
+  latency-bound decoder more than the stitch costs in order (128 x 25 M: 6.40 ms
+  in order, 6.56-7.10 split; 64 x 11 M: 1.68 vs 1.62; tools/diag/split_stitch.sh)."""
+  import os  # pylint: disable=g-import-not-at-top
+  return os.environ.get("FEDCODEC_SPLIT_STITCH", "0") != "0"
+
+
+_STITCH_STREAMS = {}
+
+
+def _stitch_stream(device):
+  key = torch.device(device).index or 0
+  if key not in _STITCH_STREAMS:
+    _STITCH_STREAMS[key] = torch.cuda.Stream(device=device)
+  return _STITCH_STREAMS[key]
 
 
 class Workspace:
@@ -190,16 +254,26 @@ def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, p
   if out is None:
     out = EncodedBatch(P, C, caps if caps is not None else [default_capacity(P)] * C, device)
   nseg = auto_segments(C, P) if segments is None else int(segments)
+  out.join(stream)  # a previous round's stitch into this batch has finished
+  out.seg = None
   if nseg > 1:
     max_cap = int(out.caps_host.max())
-    sws = _SEG_WS.get(C, P, nseg, max_cap, device)
+    split = split_stitch_wanted()
+    sws = out.seg_workspace(nseg, max_cap) if split else _SEG_WS.get(C, P, nseg, max_cap, device)
     if sws is not None:
-      _lib.call("fc_quantize_encode_segmented", _lib.ptr(ptrs), C, P, float(step), _lib.ptr(norms),
-                _lib.ptr(prescale), _lib.ptr(seeds), int(mode), nseg, max_cap, _lib.ptr(out.stream),
-                _lib.ptr(out.stream_off), _lib.ptr(out.stream_cap), _lib.ptr(out.idx), _lib.ptr(out.total_bits),
-                _lib.ptr(out.dist_part), _lib.ptr(out.nnz_part), _lib.ptr(out.overflow), _lib.ptr(sws),
-                sws.numel(), _lib.stream_handle(stream))
+      main = stream if stream is not None else torch.cuda.current_stream()
+      side = _stitch_stream(device) if split else main
+      _lib.call("fc_quantize_encode_segmented_split", _lib.ptr(ptrs), C, P, float(step), _lib.ptr(norms),
+                _lib.ptr(prescale), _lib.ptr(seeds), int(mode), nseg, max_cap, _lib.ptr(out._stream),
+                _lib.ptr(out.stream_off), _lib.ptr(out.stream_cap), _lib.ptr(out._idx), _lib.ptr(out.total_bits),
+                _lib.ptr(out._dist_part), _lib.ptr(out._nnz_part), _lib.ptr(out.overflow), _lib.ptr(sws),
+                sws.numel(), _lib.stream_handle(main), _lib.stream_handle(side))
       out.quarters = False
+      if split:
+        out.seg = (sws, nseg, max_cap)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        out._pending = ev
       return out
   ws = _WS.get(C, P, device)
   if quarter_index_wanted(C, nseg) if quarters is None else quarters:
@@ -352,6 +426,18 @@ def decode_accumulate(batch, sum_in=None, want_sum=True, out=None, step=1.0, noi
   device = batch.device
   if want_sum and sum_out is None:
     sum_out = torch.empty(batch.P, dtype=torch.int32, device=device)
+  if batch.seg is not None:  # straight from the unstitched segments (the stitch may still run)
+    ws, nseg, max_cap = batch.seg
+    if err is None:
+      err = torch.zeros(1, dtype=torch.int32, device=device)
+    elif tiles is None:
+      with torch.cuda.stream(stream):
+        err.zero_()
+    t0, t1 = (0, batch.T) if tiles is None else tiles
+    _lib.call("fc_decode_accumulate_segmented", _lib.ptr(ws), ws.numel(), batch.nclients, batch.P, int(nseg),
+              int(max_cap), int(t0), int(t1), _lib.ptr(sum_in), _lib.ptr(sum_out if want_sum else None),
+              _lib.ptr(out), float(step), _lib.ptr(noise_sum), _lib.ptr(err), _lib.stream_handle(stream))
+    return (sum_out if want_sum else None), out, err
   if batch.quarters:  # quarter-tile lane segments (fc_decode_accumulate_quarters ORs into err)
     if err is None:
       err = torch.zeros(1, dtype=torch.int32, device=device)
@@ -387,6 +473,7 @@ def decode_accumulate_scaled(batch, client_scale, out=None, fsum_in=None, stream
   Returns (out, err tensor).
   """
   _lib.require_gpu()
+  batch.join(stream)
   device = batch.device
   if out is None:
     out = torch.empty(batch.P, dtype=torch.float32, device=device)
@@ -429,6 +516,7 @@ def vote_lengths(xs, steps, seeds, mode, stream=None):
 
 def finalize(batch, stream=None):
   """Per-client float64 sum of squared error and int64 nonzero count (device)."""
+  batch.join(stream)  # the partials of a segmented batch come with its stitch
   dist = torch.empty(batch.nclients, dtype=torch.float64, device=batch.device)
   nnz = torch.empty(batch.nclients, dtype=torch.int64, device=batch.device)
   _lib.call("fc_finalize", _lib.ptr(batch.dist_part), _lib.ptr(batch.nnz_part), batch.nclients,

@@ -2291,6 +2291,12 @@ struct DecodeArgs {
   int64_t plane_stride;
   int32_t t_begin, t_end;     // tiles decoded: [t_begin, t_end)
   const uint64_t* idxq;       // nullable [nclients * T][3]: quarter-tile entries (lane segments of 256)
+  // VIRT: an unstitched segmented batch -- client c's tiles [k Tv, (k + 1) Tv) are virtual client
+  // c K + k's tiles (k < K), the rest virtual client C K + c's; stream_off / stream_cap are indexed
+  // by virtual client, idx is unused
+  const uint64_t* vidx_main;  // [C K][Tv + 1]
+  const uint64_t* vidx_rem;   // [C][Tr + 1]
+  int32_t vK, vTv, vTr;
 };
 
 // General decode of one code at absolute bit position pos straight from
@@ -2735,7 +2741,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 // (256 elements, entries from the quarter index): four times the segments in
 // flight for few clients with dense codes (config 2: 128 clients, ~10 bits per
 // element -- each lane's serial chain, not memory, bounds the decode).
-template <bool PLANE, int SPAN_ = 1, bool QTR = false>
+template <bool PLANE, int SPAN_ = 1, bool QTR = false, bool VIRT = false>
 #ifndef FC_DEC_WPE
 #define FC_DEC_WPE 5  // waves per SIMD the register budget is held to
 #endif
@@ -2768,11 +2774,30 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
     }
     const int64_t u = u0 + sub * SPAN;
     if (u < u_end) {
-      const int64_t unit_base = u * UE;
-      const int64_t uE = min<int64_t>(u + SPAN, u_end);  // segment end unit
-      const uint32_t span = (uint32_t)(uE - u) * UE;
       const int64_t t = u / UPT;
       const int qs = (int)(u - t * UPT);  // QTR: quarter of the tile
+      const int64_t uEnd = min<int64_t>(u + SPAN, u_end);  // lane segment end unit
+      // VIRT: a lane segment that straddles an encoder segment's end (a tile range
+      // starting at an odd tile) is decoded as two pieces, one per encoder segment
+      int64_t uA = uEnd;
+      if (VIRT) {
+        const int32_t tm = a.vK * a.vTv;
+        const int32_t k0 = (int32_t)t < tm ? (int32_t)t / a.vTv : a.vK;
+        if (k0 < a.vK) uA = min<int64_t>(uEnd, (int64_t)(k0 + 1) * a.vTv);
+      }
+      for (int piece = 0; piece < (VIRT ? 2 : 1); ++piece) {
+      const int64_t pu = piece ? uA : u;          // the piece's first unit
+      const int64_t uE = piece ? uEnd : uA;       // and end unit
+      if (pu >= uE) break;
+      const int64_t unit_base = pu * UE;
+      const uint32_t span = (uint32_t)(uE - pu) * UE;
+      const uint32_t paddr = my_addr + 4u * (uint32_t)((pu - u) * UE);  // the piece's accumulator
+      int32_t vk = 0, vj = 0;  // VIRT: the encoder segment holding the piece (vK: the remainder), its tile there
+      if (VIRT) {
+        const int32_t tm = a.vK * a.vTv;
+        vk = (int32_t)pu < tm ? (int32_t)pu / a.vTv : a.vK;
+        vj = (int32_t)pu - vk * a.vTv;
+      }
       for (int c = l; c < a.nclients; c += a.lanes_per_tile) {
 #if FC_DEC_ABL & 8  // diagnostics: 8 clients' streams and indexes for every lane (cache-resident reads)
         const int cc = c & 7;
@@ -2781,7 +2806,21 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
 #endif
         const int64_t ib = (int64_t)cc * (a.T + 1) + t;
         uint64_t e0, e1;
-        if (QTR) {
+        int64_t vc = cc;       // stream row (VIRT: the virtual client)
+        int64_t rel_base = unit_base;  // the index's element coordinate of the unit (VIRT: segment-local)
+        if (VIRT) {
+          const uint64_t* vi;
+          if (vk < a.vK) {
+            vc = (int64_t)cc * a.vK + vk;
+            vi = a.vidx_main + vc * (a.vTv + 1);
+          } else {
+            vc = (int64_t)a.nclients * a.vK + cc;
+            vi = a.vidx_rem + (int64_t)cc * (a.vTr + 1);
+          }
+          e0 = vi[vj];
+          e1 = vi[vj + (uE - pu)];
+          rel_base = (int64_t)vj * kTE;
+        } else if (QTR) {
           const uint64_t* q = a.idxq + 3 * ((int64_t)cc * a.T + t);
           e0 = qs == 0 ? a.idx[ib] : q[qs - 1];
           e1 = qs == 3 ? a.idx[ib + 1] : q[qs];
@@ -2789,22 +2828,23 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
           e0 = a.idx[ib];
           e1 = a.idx[ib + (uE - u)];
         }
-        const int64_t soff = a.stream_off[cc], scap = a.stream_cap[cc];
+        const int64_t soff = a.stream_off[vc], scap = a.stream_cap[vc];
         const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
         if (bend <= bstart) continue;
-        const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - unit_base);  // last nonzero, unit-relative
+        const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - rel_base);  // last nonzero, unit-relative
         int32_t* ptile = PLANE ? a.plane + (int64_t)c * a.plane_stride + unit_base : nullptr;
         const uint32_t hib = PLANE ? 4u * (uint32_t)min<int64_t>(kTE, a.P - unit_base) : 0u;
         // a wave whose segments are all long-code streams skips the table steps
         if (kDecLongBits > 0 && __ballot(bend - bstart < (uint64_t)kDecLongBits * span) == 0)
-          decode_segment<PLANE, true>(a.stream_buf + soff, scap, bstart, bend, rel, my_addr, lut, a.err, ptile, hib,
+          decode_segment<PLANE, true>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err, ptile, hib,
                                       span);
         else if (kDecStep3Bits16 > 0 && __ballot(bend - bstart >= (uint64_t)kDecStep3Bits16 * (span / 16)) == 0)
-          decode_segment<PLANE, false, true>(a.stream_buf + soff, scap, bstart, bend, rel, my_addr, lut, a.err, ptile,
+          decode_segment<PLANE, false, true>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err, ptile,
                                              hib, span);
         else
-          decode_segment<PLANE>(a.stream_buf + soff, scap, bstart, bend, rel, my_addr, lut, a.err, ptile, hib, span);
+          decode_segment<PLANE>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err, ptile, hib, span);
       }
+      }  // pieces
     }
     if (PLANE) continue;
     __syncthreads();
@@ -4172,7 +4212,7 @@ int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float 
                      const float* prescale, const int64_t* seeds, int mode, int32_t K, int64_t max_cap,
                      uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
                      int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow, void* workspace,
-                     int64_t workspace_bytes, void* stream) {
+                     int64_t workspace_bytes, void* stream, void* stitch_stream = nullptr) {
   SegLayout L;
   if (!seg_layout(nclients, P, K, max_cap, L)) return fail(-1, "segmented encode: segments below 2048 elements");
   if (!xs || !stream_buf || !stream_off || !stream_cap || !idx || !total_bits || !overflow)
@@ -4241,11 +4281,26 @@ int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float 
   }
   hipLaunchKernelGGL(k_seg_plan, dim3(nclients), dim3(64), 0, s, a);
   if (const int rc2 = check_launch("k_seg_plan")) return rc2;
+  // the stitch (bit moves, canonical index, partials) may run on a second stream,
+  // beside a decode of the unstitched segments (fc_decode_accumulate_segmented)
+  const bool split = stitch_stream && stitch_stream != stream;
+  if (split) {
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail(-10, "event create");
+    const bool ok = hipEventRecord(ev, s) == hipSuccess && hipStreamWaitEvent((hipStream_t)stitch_stream, ev, 0) == hipSuccess;
+    (void)hipEventDestroy(ev);
+    if (!ok) return fail(-10, "stitch stream ordering");
+    s = (hipStream_t)stitch_stream;
+  }
   const int64_t bpc = (max_cap / 4 + kSegWordsPerBlock - 1) / kSegWordsPerBlock;
   int dev = 0, ncu = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t cgrid = std::min<int64_t>(bpc * nclients, (int64_t)ncu * 16);
+  // beside a decode (split stitch) the copy takes a few workgroups per CU, so the
+  // decoder's workgroups stay resident
+  int64_t per_cu = split ? 2 : 16;
+  if (const char* e = getenv("FEDCODEC_SPLIT_COPY_WG")) if (split) per_cu = std::max(1, atoi(e));  // test knob
+  const int64_t cgrid = std::min<int64_t>(bpc * nclients, (int64_t)ncu * per_cu);
   hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)cgrid), dim3(256), 0, s, a, bpc);
   if (const int rc3 = check_launch("k_seg_copy")) return rc3;
   const int64_t T = tiles_for(P);
@@ -4279,7 +4334,8 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   // lanes per tile: 128 (two tiles per workgroup; measured 2-3 % faster than 256 at
   // 256 and 1024 clients, 64 is 20 % slower), fewer for few clients
   const bool plane = a.plane != nullptr;
-  const bool qtr = !plane && a.idxq != nullptr;  // quarter-tile lane segments
+  const bool virt = !plane && a.vidx_main != nullptr;  // an unstitched segmented batch
+  const bool qtr = !plane && !virt && a.idxq != nullptr;  // quarter-tile lane segments
   int span = (!plane && !qtr && nclients >= kDecSpan2Clients) ? 2 : 1;
   if (const char* e = getenv("FEDCODEC_DEC_SPAN")) span = (!plane && !qtr && atoi(e) == 2) ? 2 : 1;  // test knob
   int lpt = span == 2 ? 256 : 128;
@@ -4289,8 +4345,9 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
     if (v == 64 || v == 128 || v == 256) lpt = v;
   }
   a.lanes_per_tile = lpt;
-  void (*kern)(DecodeArgs) = plane ? k_decode<true>
-                             : qtr     ? k_decode<false, 1, true>
+  void (*kern)(DecodeArgs) = plane  ? k_decode<true>
+                             : qtr  ? k_decode<false, 1, true>
+                             : virt ? (span == 2 ? k_decode<false, 2, false, true> : k_decode<false, 1, false, true>)
                              : span == 2 ? k_decode<false, 2> : k_decode<false, 1>;
   const int ue = qtr ? kTE / 4 : kTE;  // elements per unit
   const int tpw = kDecThreads / lpt * span;  // units per workgroup
@@ -4377,6 +4434,44 @@ int fc_quantize_encode_segmented(const float* const* xs, int32_t nclients, int64
   return encode_segmented(xs, nclients, P, step, norms, prescale, seeds, mode, nseg, max_cap, stream_buf, stream_off,
                           stream_cap, idx, total_bits, dist_part, nnz_part, overflow, workspace, workspace_bytes,
                           stream);
+}
+
+int fc_quantize_encode_segmented_split(const float* const* xs, int32_t nclients, int64_t P, float step,
+                                       const float* norms, const float* prescale, const int64_t* seeds, int mode,
+                                       int32_t nseg, int64_t max_cap, uint8_t* stream_buf,
+                                       const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
+                                       int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow,
+                                       void* workspace, int64_t workspace_bytes, void* stream,
+                                       void* stitch_stream) {
+  if (mode < 0 || mode > 2) return fail(-1, "mode must be 0 (uniform), 1 (stochastic) or 2 (dithered)");
+  return encode_segmented(xs, nclients, P, step, norms, prescale, seeds, mode, nseg, max_cap, stream_buf, stream_off,
+                          stream_cap, idx, total_bits, dist_part, nnz_part, overflow, workspace, workspace_bytes,
+                          stream, stitch_stream);
+}
+
+int fc_decode_accumulate_segmented(const void* workspace, int64_t workspace_bytes, int32_t nclients, int64_t P,
+                                   int32_t nseg, int64_t max_cap, int32_t tile_begin, int32_t tile_end,
+                                   const int32_t* sum_in, int32_t* sum_out, float* out, float step,
+                                   const float* noise_sum, int32_t* err, void* stream) {
+  if (!sum_out && !out) return fail(-1, "one of sum_out / out required");
+  SegLayout L;
+  if (!seg_layout(nclients, P, nseg, max_cap, L)) return fail(-1, "segmented decode: segments below 2048 elements");
+  if (!workspace || workspace_bytes < L.total || ((uintptr_t)workspace & 255))
+    return fail(-1, "segmented workspace too small or not 256-byte aligned");
+  const uint8_t* w = (const uint8_t*)workspace;
+  DecodeArgs a{};
+  a.sum_in = sum_in;
+  a.sum_out = sum_out;
+  a.out = out;
+  a.step = step;
+  a.noise_sum = noise_sum;
+  a.vidx_main = (const uint64_t*)(w + L.o_vidx_main);
+  a.vidx_rem = (const uint64_t*)(w + L.o_vidx_rem);
+  a.vK = nseg;
+  a.vTv = L.Tv;
+  a.vTr = L.Tr;
+  return decode_common(a, w + L.o_vstream, (const int64_t*)(w + L.o_vsoff), (const int64_t*)(w + L.o_vscap),
+                       a.vidx_main, nclients, P, err, stream, tile_begin, tile_end, false);
 }
 
 int fc_quantize_encode_hinted(const float* const* xs, int32_t nclients, int64_t P, float step,

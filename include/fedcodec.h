@@ -147,6 +147,34 @@ int fc_quantize_encode_segmented(const float* const* xs, int32_t nclients, int64
                                  int32_t* overflow, void* workspace, int64_t workspace_bytes,
                                  void* stream);
 
+/* fc_quantize_encode_segmented with the stitch on a second stream: the segments'
+ * encode and the plan (total_bits, overflow) run on `stream`; the bit moves into
+ * the canonical streams, the canonical idx and the per-tile partials on
+ * `stitch_stream` (ordered after the plan; the caller joins it before reading
+ * stream_buf, idx, dist_part or nnz_part).  Meanwhile
+ * fc_decode_accumulate_segmented can decode the unstitched segments on `stream`
+ * from the same workspace (kept unchanged until both are done).  stitch_stream ==
+ * stream or NULL: exactly fc_quantize_encode_segmented. */
+int fc_quantize_encode_segmented_split(const float* const* xs, int32_t nclients, int64_t P, float step,
+                                       const float* norms, const float* prescale, const int64_t* seeds,
+                                       int mode, int32_t nseg, int64_t max_cap, uint8_t* stream_buf,
+                                       const int64_t* stream_off, const int64_t* stream_cap,
+                                       uint64_t* idx, int64_t* total_bits, float* dist_part,
+                                       int32_t* nnz_part, int32_t* overflow, void* workspace,
+                                       int64_t workspace_bytes, void* stream, void* stitch_stream);
+
+/* Decode + client sum of a segmented batch straight from its segments (the
+ * workspace of the fc_quantize_encode_segmented(_split) call that made them, same
+ * nclients / P / nseg / max_cap): each segment's code and index are the client's
+ * code and index for its element range, so the results equal
+ * fc_decode_accumulate_tiles on the stitched batch bit for bit.  Tile range and
+ * err as fc_decode_accumulate_tiles (err is OR'ed into). */
+int fc_decode_accumulate_segmented(const void* workspace, int64_t workspace_bytes, int32_t nclients,
+                                   int64_t P, int32_t nseg, int64_t max_cap, int32_t tile_begin,
+                                   int32_t tile_end, const int32_t* sum_in, int32_t* sum_out,
+                                   float* out, float step, const float* noise_sum, int32_t* err,
+                                   void* stream);
+
 /* fc_quantize_encode plus a quarter-tile decoder index: idxq = device
  * uint64[nclients * fc_num_tiles(P) * 3], entry 3 (c * tiles + t) + s - 1 = the
  * decoder entry (bit offset | 1 + last nonzero before, << 36) of elements

@@ -16,6 +16,14 @@ from oracle import codec as ocodec
 from oracle import quantize_utils as oq
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["1", "0"], ids=["split", "inorder"])
+def _stitch_mode(monkeypatch, request):
+  """Both stitch orders: on a second stream beside the decode of the unstitched
+  segments (default), and in order before anything else."""
+  monkeypatch.setenv("FEDCODEC_SPLIT_STITCH", request.param)
+  return request.param
 F32 = np.float32
 MODES = {"uniform": _lib.UNIFORM, "stochastic": _lib.STOCHASTIC, "dithered": _lib.DITHERED}
 ORACLE_Q = {"uniform": lambda x, s, sd: oq.uniform_quantize(x, s), "stochastic": oq.stochastic_quantize,
@@ -138,3 +146,30 @@ def test_segmented_at_the_8gpu_share_shape(gpu):
   assert int(e1.item()) == 0 and int(e2.item()) == 0 and torch.equal(s1, s2)
   del rows, seg, one
   torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("span", ["1", "2"])
+def test_unstitched_decode_tile_ranges(gpu, span, monkeypatch, _stitch_mode):
+  """Tile-range decodes (the multi-GPU slabs) straight from the segments, before the
+  stitch is joined: ranges starting and ending at odd tiles and inside segments,
+  two-tile lane segments that would straddle a segment end -- equal to the one-piece
+  batch's decode."""
+  monkeypatch.setenv("FEDCODEC_DEC_SPAN", span)
+  C, P, K = 3, 150_001, 5  # 28,672-element segments (28 tiles) + a 6,641-element remainder
+  xs = _data("gauss", C, P, seed=31)
+  rows = [torch.from_numpy(x).to(gpu) for x in xs]
+  seeds = torch.tensor([[c, 2 * c] for c in range(C)], dtype=torch.int64)
+  caps = [codec.worst_case_capacity(P) // 4] * C
+  seg = codec.quantize_encode(rows, 0.5, seeds, _lib.STOCHASTIC, caps=caps, segments=K)
+  one = codec.quantize_encode(rows, 0.5, seeds, _lib.STOCHASTIC, caps=caps, segments=1)
+  assert (seg.seg is not None) == (_stitch_mode == "1")  # split: decoded before the stitch is joined
+  T = seg.T
+  want, _, e1 = codec.decode_accumulate(one)
+  part = torch.full((P,), 77, dtype=torch.int32, device=gpu)
+  err = torch.zeros(1, dtype=torch.int32, device=gpu)
+  bounds = [0, 3, 27, 29, 57, 84, 85, 140, T]
+  for tb, te in zip(bounds[:-1], bounds[1:]):
+    codec.decode_accumulate(seg, sum_out=part, err=err, tiles=(tb, te))
+  assert int(err.item()) == 0 and int(e1.item()) == 0
+  np.testing.assert_array_equal(part.cpu().numpy(), want.cpu().numpy())
+  _same(seg, one)
