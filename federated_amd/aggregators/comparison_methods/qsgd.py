@@ -77,7 +77,12 @@ class QSGDFactory(tc.UnweightedAggregationFactory):
       steps_dev = torch.from_numpy(steps).cuda()
       # client step = steps[c] * 1.0 (exact); stochastic rounding (:68-69)
       batch = codec.quantize_encode_checked(rows, 1.0, seeds, _lib.STOCHASTIC, norms=steps_dev)
-      out, err = codec.decode_accumulate_scaled(batch, steps_dev)                      # :85-112
+      # |q| <= num_steps + 1 whenever every client step is positive and finite (|x| <=
+      # ||x||_2): the server's q rows can then be int8
+      qmax = int(np.ceil(num_steps)) + 1
+      if not (np.all(steps > 0) and np.all(np.isfinite(steps)) and qmax <= 127):
+        qmax = None
+      out, err = codec.decode_accumulate_scaled(batch, steps_dev, qmax=qmax)           # :85-112
       dist, nnz = codec.finalize(batch)
       if int(err.item()):
         raise RuntimeError("malformed run-length gamma code")

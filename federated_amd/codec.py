@@ -466,11 +466,13 @@ def decode_accumulate(batch, sum_in=None, want_sum=True, out=None, step=1.0, noi
 
 
 def decode_accumulate_scaled(batch, client_scale, out=None, fsum_in=None, stream=None, err=None,
-                             workspace=None):
+                             workspace=None, qmax=None):
   """QSGD server sum: out = (fsum_in or 0) + float(q_c) * client_scale[c], added in
   client order in float32 (the reference's sequential sum, bit for bit).
 
-  Returns (out, err tensor).
+  ``qmax``: a bound the caller guarantees on every |q| (QSGD: num_steps + 1); at
+  most 127 keeps the clients' q rows as int8 (fc_decode_accumulate_scaled_bounded:
+  a quarter of the rows' traffic; a larger value sets err).  Returns (out, err).
   """
   _lib.require_gpu()
   batch.join(stream)
@@ -484,9 +486,9 @@ def decode_accumulate_scaled(batch, client_scale, out=None, fsum_in=None, stream
   if workspace is None:
     nbytes = int(_lib.load().fc_decode_scaled_workspace_bytes(int(batch.nclients), int(batch.P)))
     workspace = torch.empty(nbytes, dtype=torch.uint8, device=device)
-  _lib.call("fc_decode_accumulate_scaled", _lib.ptr(batch.stream), _lib.ptr(batch.stream_off),
+  _lib.call("fc_decode_accumulate_scaled_bounded", _lib.ptr(batch.stream), _lib.ptr(batch.stream_off),
             _lib.ptr(batch.stream_cap), _lib.ptr(batch.idx), batch.nclients, batch.P,
-            _lib.ptr(client_scale), _lib.ptr(fsum_in), _lib.ptr(out), _lib.ptr(err),
+            _lib.ptr(client_scale), _lib.ptr(fsum_in), _lib.ptr(out), _lib.ptr(err), int(qmax or 0),
             _lib.ptr(workspace), workspace.numel(), _lib.stream_handle(stream))
   return out, err
 

@@ -2287,8 +2287,9 @@ struct DecodeArgs {
   float step;
   const float* noise_sum;
   int32_t* err;
-  int32_t* plane;             // PLANE: q of each client, row c at plane + c * plane_stride
+  int32_t* plane;             // PLANE: q of each client, row c at plane + c * plane_stride (elements)
   int64_t plane_stride;
+  int32_t plane8;             // the rows are int8 (|q| <= 127 declared)
   int32_t t_begin, t_end;     // tiles decoded: [t_begin, t_end)
   const uint64_t* idxq;       // nullable [nclients * T][3]: quarter-tile entries (lane segments of 256)
   // VIRT: an unstitched segmented batch -- client c's tiles [k Tv, (k + 1) Tv) are virtual client
@@ -2555,12 +2556,19 @@ constexpr int kDecSpan2Clients = 256;
 typedef __attribute__((address_space(3))) int32_t* lds_iptr;
 
 // Accumulator add at LDS byte address a (int32 client sum), or (PLANE, the
-// QSGD server sum) a store of the value into the client's q row at byte offset a
+// QSGD server sum) a store of the value into the client's q row at element a / 4
 // of the tile -- only nonzero values (a no-op zero add may repeat the previous
 // code's slot or point past the tile) inside the tile's valid bytes `hib`.
-template <bool PLANE>
-__device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, int32_t* ptile, uint32_t hib) {
-  if (PLANE) {
+// PLANE 1: int32 rows; 2: int8 rows (|q| <= 127 declared by the caller; a larger
+// value sets err).
+template <int PLANE>
+__device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, int32_t* ptile, uint32_t hib, int32_t* err = nullptr) {
+  if (PLANE == 2) {
+    if (v != 0 && a < hib) {
+      if (v > 127 || v < -127) atomicOr(err, 1);
+      ((int8_t*)ptile)[a >> 2] = (int8_t)v;
+    }
+  } else if (PLANE) {
     if (v != 0 && a < hib) ptile[a >> 2] = v;
   } else {
 #if FC_DEC_ABL & 1
@@ -2583,7 +2591,7 @@ __device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, int32_t* ptile
 // window bits in the next arithmetic slot (longer than 32 bits: slow_code, then
 // the reader restarts).  The window holds >= 33 valid bits when an iteration
 // starts.
-template <bool PLANE, bool LONG = false, bool STEP3 = false>
+template <int PLANE, bool LONG = false, bool STEP3 = false>
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
                                                uint64_t b1, int32_t rel, uint32_t my_addr,
                                                const uint32_t* lut, int32_t* err, int32_t* ptile,
@@ -2634,9 +2642,9 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       // entry takes a code there
       const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
       relb += e & 0x7Fu;
-      acc_add_at<PLANE>(relb, ((int32_t)(e << 12)) >> 26, ptile, hib);
+      acc_add_at<PLANE>(relb, ((int32_t)(e << 12)) >> 26, ptile, hib, err);
       relb += (e >> 7) & 0x7Fu;
-      acc_add_at<PLANE>(relb, ((int32_t)(e << 6)) >> 26, ptile, hib);
+      acc_add_at<PLANE>(relb, ((int32_t)(e << 6)) >> 26, ptile, hib, err);
       const uint32_t L = e >> 26;
       r.win <<= L;
       cons += (int32_t)L;
@@ -2649,9 +2657,9 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
       e = ok3 ? e : 0u;
       relb += e & 0x7Fu;
-      acc_add_at<PLANE>(relb, ((int32_t)(e << 12)) >> 26, ptile, hib);
+      acc_add_at<PLANE>(relb, ((int32_t)(e << 12)) >> 26, ptile, hib, err);
       relb += (e >> 7) & 0x7Fu;
-      acc_add_at<PLANE>(relb, ((int32_t)(e << 6)) >> 26, ptile, hib);
+      acc_add_at<PLANE>(relb, ((int32_t)(e << 6)) >> 26, ptile, hib, err);
       const uint32_t L = e >> 26;
       r.win <<= L;
       cons += (int32_t)L;
@@ -2701,7 +2709,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       const uint32_t rel_new = (uint32_t)(rel_now + (int32_t)d);
       bad |= rel_new >= span ? 1u : 0u;
       relb = my_addr + 4u * min(rel_new, span - 1);
-      acc_add_at<PLANE>(relb, v, ptile, hib);
+      acc_add_at<PLANE>(relb, v, ptile, hib, err);
       cons += (int32_t)L;
     }
 #if FC_DEC_SEL_REFILL
@@ -2741,7 +2749,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 // (256 elements, entries from the quarter index): four times the segments in
 // flight for few clients with dense codes (config 2: 128 clients, ~10 bits per
 // element -- each lane's serial chain, not memory, bounds the decode).
-template <bool PLANE, int SPAN_ = 1, bool QTR = false, bool VIRT = false>
+template <int PLANE, int SPAN_ = 1, bool QTR = false, bool VIRT = false>
 #ifndef FC_DEC_WPE
 #define FC_DEC_WPE 5  // waves per SIMD the register budget is held to
 #endif
@@ -2832,7 +2840,9 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
         const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
         if (bend <= bstart) continue;
         const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - rel_base);  // last nonzero, unit-relative
-        int32_t* ptile = PLANE ? a.plane + (int64_t)c * a.plane_stride + unit_base : nullptr;
+        int32_t* ptile = PLANE == 2 ? (int32_t*)((int8_t*)a.plane + (int64_t)c * a.plane_stride + unit_base)
+                       : PLANE    ? a.plane + (int64_t)c * a.plane_stride + unit_base
+                                  : nullptr;
         const uint32_t hib = PLANE ? 4u * (uint32_t)min<int64_t>(kTE, a.P - unit_base) : 0u;
         // a wave whose segments are all long-code streams skips the table steps
         if (kDecLongBits > 0 && __ballot(bend - bstart < (uint64_t)kDecLongBits * span) == 0)
@@ -2899,7 +2909,9 @@ __global__ void k_dequantize(const int32_t* __restrict__ s, int64_t P, float ste
 // scale[c] for the clients of the plane rows in client order, float32 with no
 // contraction -- the reference's sequential client-order sum, bit for bit.  One
 // thread per 4 elements (rows padded to a multiple of 4 elements).
-__global__ __launch_bounds__(256) void k_sum_planes(const int32_t* __restrict__ planes, int64_t stride, int32_t n,
+// QT int8_t: rows of bytes (4 per 32-bit load, sign-extended).
+template <typename QT>
+__global__ __launch_bounds__(256) void k_sum_planes(const QT* __restrict__ planes, int64_t stride, int32_t n,
                                                     int64_t P, const float* __restrict__ scale,
                                                     const float* in, float* out) {
   const int64_t e0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
@@ -2909,7 +2921,13 @@ __global__ __launch_bounds__(256) void k_sum_planes(const int32_t* __restrict__ 
   if (in)
     for (int k = 0; k < m; ++k) acc[k] = in[e0 + k];
   for (int c = 0; c < n; ++c) {
-    const int4 q = *(const int4*)(planes + (int64_t)c * stride + e0);
+    int4 q;
+    if constexpr (sizeof(QT) == 1) {
+      const uint32_t w = *(const uint32_t*)(planes + (int64_t)c * stride + e0);
+      q = make_int4((int8_t)(w & 0xFFu), (int8_t)((w >> 8) & 0xFFu), (int8_t)((w >> 16) & 0xFFu), (int8_t)(w >> 24));
+    } else {
+      q = *(const int4*)(planes + (int64_t)c * stride + e0);
+    }
     const float sc = scale[c];
     acc[0] = acc[0] + (float)q.x * sc;
     acc[1] = acc[1] + (float)q.y * sc;
@@ -4345,10 +4363,10 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
     if (v == 64 || v == 128 || v == 256) lpt = v;
   }
   a.lanes_per_tile = lpt;
-  void (*kern)(DecodeArgs) = plane  ? k_decode<true>
-                             : qtr  ? k_decode<false, 1, true>
-                             : virt ? (span == 2 ? k_decode<false, 2, false, true> : k_decode<false, 1, false, true>)
-                             : span == 2 ? k_decode<false, 2> : k_decode<false, 1>;
+  void (*kern)(DecodeArgs) = plane  ? (a.plane8 ? k_decode<2> : k_decode<1>)
+                             : qtr  ? k_decode<0, 1, true>
+                             : virt ? (span == 2 ? k_decode<0, 2, false, true> : k_decode<0, 1, false, true>)
+                             : span == 2 ? k_decode<0, 2> : k_decode<0, 1>;
   const int ue = qtr ? kTE / 4 : kTE;  // elements per unit
   const int tpw = kDecThreads / lpt * span;  // units per workgroup
   const size_t lds = plane ? 0 : (size_t)tpw * ue * sizeof(int32_t);  // + the static kLutSize-word table
@@ -4560,16 +4578,19 @@ int64_t fc_decode_scaled_workspace_bytes(int32_t nclients, int64_t P) {
   return group * row;
 }
 
-int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream_off,
-                                const int64_t* stream_cap, const uint64_t* idx, int32_t nclients, int64_t P,
-                                const float* client_scale, const float* fsum_in, float* out, int32_t* err,
-                                void* workspace, int64_t workspace_bytes, void* stream) {
+int fc_decode_accumulate_scaled_bounded(const uint8_t* stream_buf, const int64_t* stream_off,
+                                        const int64_t* stream_cap, const uint64_t* idx, int32_t nclients, int64_t P,
+                                        const float* client_scale, const float* fsum_in, float* out, int32_t* err,
+                                        int32_t qmax, void* workspace, int64_t workspace_bytes, void* stream) {
   if (!out || !client_scale || !workspace) return fail(-1, "null required pointer");
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
   if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
   if ((uintptr_t)workspace & 15u) return fail(-1, "workspace must be 16-byte aligned");
-  const int64_t stride = (P + 3) & ~(int64_t)3;
-  const int64_t group = std::min<int64_t>(nclients, workspace_bytes / (4 * stride));
+  // |q| <= 127 declared: int8 rows (a quarter of the rows' memset / write / read traffic)
+  const bool q8 = qmax > 0 && qmax <= 127;
+  const int64_t eb = q8 ? 1 : 4;
+  const int64_t stride = q8 ? (P + 15) & ~(int64_t)15 : (P + 3) & ~(int64_t)3;
+  const int64_t group = std::min<int64_t>(nclients, workspace_bytes / (eb * stride));
   if (group < 1) return fail(-1, "workspace smaller than one client row (fc_decode_scaled_workspace_bytes)");
   const int64_t T = tiles_for(P);
   hipStream_t s = (hipStream_t)stream;
@@ -4577,20 +4598,33 @@ int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream
   // float32 sum in client order (the first group starts from fsum_in, or zero)
   for (int64_t c0 = 0; c0 < nclients; c0 += group) {
     const int32_t n = (int32_t)std::min<int64_t>(group, nclients - c0);
-    if (hipMemsetAsync(workspace, 0, (size_t)n * 4 * stride, s) != hipSuccess) return fail(-10, "memset planes");
+    if (hipMemsetAsync(workspace, 0, (size_t)(n * eb * stride), s) != hipSuccess) return fail(-10, "memset planes");
     DecodeArgs a{};
     a.plane = (int32_t*)workspace;
     a.plane_stride = stride;
+    a.plane8 = q8 ? 1 : 0;
     const int rc = decode_common(a, stream_buf, stream_off + c0, stream_cap + c0, idx + c0 * (T + 1), n, P, err,
                                  stream, 0, -1, c0 == 0);
     if (rc) return rc;
     const int64_t thr = (P + 3) / 4;
-    hipLaunchKernelGGL(k_sum_planes, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, (const int32_t*)workspace,
-                       stride, n, P, client_scale + c0, c0 == 0 ? fsum_in : out, out);
+    if (q8)
+      hipLaunchKernelGGL(k_sum_planes<int8_t>, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s,
+                         (const int8_t*)workspace, stride, n, P, client_scale + c0, c0 == 0 ? fsum_in : out, out);
+    else
+      hipLaunchKernelGGL(k_sum_planes<int32_t>, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s,
+                         (const int32_t*)workspace, stride, n, P, client_scale + c0, c0 == 0 ? fsum_in : out, out);
     const int rs = check_launch("k_sum_planes");
     if (rs) return rs;
   }
   return 0;
+}
+
+int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream_off,
+                                const int64_t* stream_cap, const uint64_t* idx, int32_t nclients, int64_t P,
+                                const float* client_scale, const float* fsum_in, float* out, int32_t* err,
+                                void* workspace, int64_t workspace_bytes, void* stream) {
+  return fc_decode_accumulate_scaled_bounded(stream_buf, stream_off, stream_cap, idx, nclients, P, client_scale,
+                                             fsum_in, out, err, 0, workspace, workspace_bytes, stream);
 }
 
 int64_t fc_vote_workspace_bytes(int32_t nclients, int64_t P, int32_t K) {

@@ -245,6 +245,17 @@ int fc_decode_accumulate_scaled(const uint8_t* stream_buf, const int64_t* stream
                                 float* out, int32_t* err, void* workspace, int64_t workspace_bytes,
                                 void* stream);
 
+/* fc_decode_accumulate_scaled with a caller-guaranteed bound qmax on every |q|
+ * (QSGD: num_steps + 1, since |x| <= ||x||_2).  qmax in [1, 127]: the client q rows
+ * are int8 (a quarter of the rows' memset / write / read traffic; a decoded value
+ * beyond 127 sets err); otherwise (qmax <= 0 or > 127) exactly
+ * fc_decode_accumulate_scaled.  Same float32 client-order sum bit for bit. */
+int fc_decode_accumulate_scaled_bounded(const uint8_t* stream_buf, const int64_t* stream_off,
+                                        const int64_t* stream_cap, const uint64_t* idx,
+                                        int32_t nclients, int64_t P, const float* client_scale,
+                                        const float* fsum_in, float* out, int32_t* err, int32_t qmax,
+                                        void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Step-size vote: for each client c and option k (steps = device float[K]),
  * bits[c*K + k] = exact run-length-gamma code length (bits) of quantizing x_c
  * with steps[k] (rounding `mode`, TF stream of seeds[c], the same draw for every

@@ -243,9 +243,11 @@ def test_qsgd_matches_oracle(gpu, P, C):
   np.testing.assert_array_equal(out2.result, out.result)
 
 
+@pytest.mark.parametrize("qmax", [None, 41, 127], ids=["int32rows", "int8rows41", "int8rows127"])
 @pytest.mark.parametrize("P,C,group", [(4099, 5, 2), (2048, 300, 7), (1025, 3, 3)])
-def test_decode_scaled_client_order(gpu, P, C, group):
-  """fc_decode_accumulate_scaled in client groups (a workspace of `group` rows):
+def test_decode_scaled_client_order(gpu, P, C, group, qmax):
+  """fc_decode_accumulate_scaled in client groups (a workspace of `group` int32
+  rows; with a bound qmax <= 127 the rows are int8, four times as many per group):
   acc = fsum_in, then acc + f32(q_c) * s_c in client order, bit for bit."""
   rng = np.random.default_rng(P * 7 + C)
   qs = [rng.integers(-40, 41, P).astype(np.int32) * (rng.random(P) < 0.6) for _ in range(C)]
@@ -255,12 +257,26 @@ def test_decode_scaled_client_order(gpu, P, C, group):
   fin = rng.standard_normal(P).astype(np.float32)
   stride = (P + 3) // 4 * 4
   ws = torch.empty(group * stride * 4, dtype=torch.uint8, device=gpu)
-  out, err = codec.decode_accumulate_scaled(batch, scale, fsum_in=torch.from_numpy(fin).to(gpu), workspace=ws)
+  out, err = codec.decode_accumulate_scaled(batch, scale, fsum_in=torch.from_numpy(fin).to(gpu), workspace=ws,
+                                            qmax=qmax)
   assert int(err.item()) == 0
   acc = fin.copy()
   for c in range(C):
     acc = (acc + (qs[c].astype(np.float32) * scale[c]).astype(np.float32)).astype(np.float32)
   np.testing.assert_array_equal(out.cpu().numpy(), acc)
+
+
+def test_decode_scaled_int8_rows_flag_values_past_the_bound(gpu):
+  """A declared bound the codes break (|q| = 200 > 127) is reported through err."""
+  P = 3000
+  q = np.zeros(P, np.int32)
+  q[[5, 1000, 2999]] = [3, -200, 7]
+  batch = codec.rlgamma_encode([torch.from_numpy(q).to(gpu)])
+  _, err = codec.decode_accumulate_scaled(batch, np.array([0.5], np.float32), qmax=127)
+  assert int(err.item()) != 0
+  out, err = codec.decode_accumulate_scaled(batch, np.array([0.5], np.float32))
+  assert int(err.item()) == 0
+  np.testing.assert_array_equal(out.cpu().numpy(), q.astype(np.float32) * np.float32(0.5))
 
 
 def test_qsgd_codes_bit_exact(gpu):

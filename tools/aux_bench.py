@@ -57,5 +57,7 @@ ws = torch.empty(int(_lib.load().fc_decode_scaled_workspace_bytes(C, P)), dtype=
 qout = torch.empty(P, dtype=torch.float32, device=dev)
 timed("qsgd decode+ordered sum (C x 25M)", lambda: codec.decode_accumulate_scaled(qb, steps, out=qout, workspace=ws),
       code_bytes + C * P * 8)
+timed("qsgd decode+ordered sum, int8 rows", lambda: codec.decode_accumulate_scaled(qb, steps, out=qout, workspace=ws,
+                                                                              qmax=17), code_bytes + C * P * 3)
 timed("int32 sum decode, same codes", lambda: codec.decode_accumulate(qb, want_sum=False, out=qout, step=1.0),
       code_bytes + P * 4)
