@@ -2365,6 +2365,9 @@ __device__ __noinline__ CodeVal slow_code(const uint8_t* base, int64_t cap, uint
 #ifndef FC_DEC_ABL
 #define FC_DEC_ABL 0  // decoder ablation bits (diagnostics only): 1 sums one bank per lane, 2 no sums, 8 eight clients' streams for all lanes
 #endif
+#ifndef FC_DEC_REPL
+#define FC_DEC_REPL 1  // accumulator copies per workgroup (1 or 2; A/B knob)
+#endif
 #ifndef FC_DEC_BATCH
 #define FC_DEC_BATCH 4
 #endif
@@ -2768,7 +2771,11 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
   for (int i = tid; i < kLutSize; i += kDecThreads) lut[i] = lut_entry((uint32_t)i);
   const int sub = tid / a.lanes_per_tile;
   const int l = tid - sub * a.lanes_per_tile;
-  const uint32_t my_addr = PLANE ? 0u : (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * SPAN * UE);
+  // FC_DEC_REPL accumulator copies (lane parity picks one, the copies one bank apart):
+  // fewer same-bank atomics from lanes at the same tile position
+  const int rstride = units_per_wg * UE + 1;  // words between copies
+  const uint32_t my_addr =
+      PLANE ? 0u : (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * SPAN * UE + (FC_DEC_REPL > 1 ? (l & 1) * rstride : 0));
   const int64_t e_end = min(a.P, (int64_t)a.t_end * kTE);  // elements this launch writes
   const int64_t u_begin = (int64_t)a.t_begin * UPT;
   const int64_t u_end = (e_end + UE - 1) / UE;  // units holding elements of the range
@@ -2777,7 +2784,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
   for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int64_t u0 = u_begin + grp * units_per_wg;
     if (!PLANE) {
-      for (int i = tid; i < units_per_wg * UE; i += kDecThreads) acc[i] = 0;
+      for (int i = tid; i < (FC_DEC_REPL > 1 ? 2 * rstride : units_per_wg * UE); i += kDecThreads) acc[i] = 0;
       __syncthreads();
     }
     const int64_t u = u0 + sub * SPAN;
@@ -2862,6 +2869,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
       const int64_t e = u0 * UE + i;
       if (e >= e_end) break;
       int32_t v = acc[i];
+      if (FC_DEC_REPL > 1) v = (int32_t)((uint32_t)v + (uint32_t)acc[i + rstride]);
       if (a.sum_in) v = (int32_t)((uint32_t)v + (uint32_t)a.sum_in[e]);
       if (a.sum_out) a.sum_out[e] = v;
       if (a.out) {
@@ -4369,7 +4377,8 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
                              : span == 2 ? k_decode<0, 2> : k_decode<0, 1>;
   const int ue = qtr ? kTE / 4 : kTE;  // elements per unit
   const int tpw = kDecThreads / lpt * span;  // units per workgroup
-  const size_t lds = plane ? 0 : (size_t)tpw * ue * sizeof(int32_t);  // + the static kLutSize-word table
+  const size_t lds = plane ? 0 : (size_t)(FC_DEC_REPL > 1 ? 2 * (tpw * ue + 1) : tpw * ue) * sizeof(int32_t);
+  // (+ the static kLutSize-word table)
   int dev = 0, ncu = 256, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
