@@ -861,6 +861,9 @@ __device__ __forceinline__ float div_step(float x, float step, float y) {
 #ifndef FC_NZ_BITS
 #define FC_NZ_BITS 1  // chunk first / last nonzero by bit scans of a nonzero mask (0: select chains)
 #endif
+#ifndef FC_NZ_ADDC
+#define FC_NZ_ADDC 1  // that mask by add-with-carry steps from the nonzero lane masks (0: selects and ORs)
+#endif
 template <int MODE, int DIV, bool PRE, bool MASK = false, bool PAIR = false>
 __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t g,
                                                      const uint32_t (&r4)[4], int32_t rel0,
@@ -906,10 +909,29 @@ __device__ __forceinline__ ChunkCode quant_code_fast(const ClientQ& cq, uint32_t
 #if FC_NZ_BITS
   // from a 4-bit mask of the nonzeros, by bit scans: the select chains below came
   // out as divergent branches (exec-mask juggling around single adds)
+#if FC_NZ_ADDC
+  // the mask from the nonzero tests' lane masks (the SGPR pairs the nnz ballots
+  // already hold): one select and three add-with-carry steps, m = 2m + carry_k,
+  // instead of four selects and the ORs
+  uint32_t nzm;
+  {
+    const uint64_t b0 = __ballot(nz[0]), b1 = __ballot(nz[1]), b2 = __ballot(nz[2]), b3 = __ballot(nz[3]);
+    uint64_t cj;
+    nzm = nz[3] ? 1u : 0u;
+    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(nzm), "=s"(cj) : "v"(nzm), "s"(b2));
+    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(nzm), "=s"(cj) : "v"(nzm), "s"(b1));
+    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(nzm), "=s"(cj) : "v"(nzm), "s"(b0));
+  }
+#else
   uint32_t nzm = (nz[0] ? 1u : 0u) | (nz[1] ? 2u : 0u) | (nz[2] ? 4u : 0u) | (nz[3] ? 8u : 0u);
   asm volatile("" : "+v"(nzm));
+#endif
+#if FC_ABL & 8192  // diagnostics: no chunk first / last nonzero (wrong stream)
+  int32_t cfirst = rel0 + (int32_t)(nzm & 1u), clast = rel0 + 3;
+#else
   int32_t cfirst = nzm ? rel0 + (int32_t)__builtin_ctz(nzm) : -1;
   int32_t clast = nzm ? rel0 + 31 - (int32_t)__builtin_clz(nzm) : -1;
+#endif
   asm volatile("" : "+v"(cfirst), "+v"(clast));
 #else
   int32_t cfirst = nz[0] ? rel0 : (nz[1] ? rel0 + 1 : (nz[2] ? rel0 + 2 : (nz[3] ? rel0 + 3 : -1)));
@@ -1055,6 +1077,173 @@ __device__ __forceinline__ void chunk_prepend(ChunkCode& r, int32_t prev) {
     r.acc |= (uint64_t)d << (r.len & 63u);
     r.len += rl;
   }
+}
+
+// Chained pair table (k_encode2, FC_PAIR_CHAIN): the run state crosses the
+// lane's chunks, so a chunk's first nonzero takes its run code from the table
+// like every other nonzero, and no per-chunk first / last nonzero or prepend is
+// computed.  Entry (s << 8) | ((qb & 15) << 4) | (qa & 15): s = distance from the
+// lane's last nonzero to qa, 1..6; 0 no nonzero yet in the lane (the lane's first
+// run code comes from the wave scan); 7 "far" (>= 7: a nonzero here is coded
+// without its run code and flagged, and the caller prepends the exact one).
+// [31:14] code, [13] flag, [12:10] the state for the next pair (already the
+// byte offset of its table region), [4:0] length.
+constexpr int kChainStates = 8;
+constexpr uint32_t kChainFar = 7;
+constexpr int kChainLut = kChainStates * 256;
+constexpr uint32_t kChainFlag = 1u << 13;
+constexpr uint32_t kChainState = 7u << 10;
+__device__ __forceinline__ uint32_t pair_chain_entry(uint32_t i) {
+  const uint32_t s = i >> 8;
+  const int32_t qa = ((int32_t)(i << 28)) >> 28, qb = ((int32_t)(i << 24)) >> 28;
+  if (qa < -7 || qb < -7) return 0u;  // |q| = 8: never looked up
+  uint32_t code = 0, len = 0, flag = 0;
+  const int32_t qs[2] = {qa, qb};
+  uint32_t run = s;
+  for (int k = 0; k < 2; ++k) {
+    const int32_t q = qs[k];
+    if (q != 0) {
+      const uint32_t m = (uint32_t)(q < 0 ? -q : q);
+      const uint32_t ml = glen(m);
+      uint32_t c = ((uint32_t)(q > 0) << ml) | m, L = 1u + ml;
+      if (run == kChainFar) {
+        flag = 1;  // the caller prepends the exact run code (only a chunk's first nonzero can be far)
+      } else if (run) {
+        c |= run << L;
+        L += glen(run);
+      }
+      code = (code << L) | c;
+      len += L;
+      run = 1;
+    } else if (run) {
+      run = min(run + 1u, kChainFar);
+    }
+  }
+  return (code << 14) | (flag << 13) | (run << 10) | len;
+}
+
+struct ChainCode {
+  uint64_t acc;
+  uint32_t len;
+  uint32_t lng;  // a code > 32 bits, |r| >= 8192 / Inf / NaN, or more than 64 bits
+  uint32_t nzm;  // nonzero mask of the chunk (bit k: element k)
+  uint32_t pre;  // the chunk's first nonzero still needs its run code (a nonzero before it in the lane)
+};
+
+// quant_code_fast for the chained table: the same quantiser, numerics and
+// counts; sst holds the run state as a byte offset into the chained table
+// (state << 10) and is advanced past the chunk.
+template <int MODE, int DIV, bool PRE, bool MASK = false>
+__device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_t g, const uint32_t (&r4)[4],
+                                                      float& dist, int32_t& nnz, const uint32_t* clut,
+                                                      const uint32_t* plut, uint32_t& sst, int32_t nvalid = 4) {
+  uint4 rb = make_uint4(0, 0, 0, 0);
+  if (FC_ABL & 8) {
+    rb.x = g * 2654435761u; rb.y = rb.x ^ 0x9E3779B9u; rb.z = rb.x + cq.key.k0; rb.w = rb.y ^ cq.key.k1;
+  } else if (MODE != FC_UNIFORM) {
+    rb = philox_group_u(cq.key, g);
+  }
+  const uint32_t rbits[4] = {rb.x, rb.y, rb.z, rb.w};
+  float q[4];
+  bool nz[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float xv = __uint_as_float(r4[k]);
+    if (PRE) xv = (xv * cq.s0) * cq.s1;
+    const float sc = div_step<DIV>(xv, cq.step, cq.rcp);
+    float r, noise = 0.0f;
+    if (MODE == FC_UNIFORM) {
+      r = rintf(sc);
+    } else if (MODE == FC_STOCHASTIC) {
+      const float fl = floorf(sc);
+      r = (u01(rbits[k]) <= sc - fl) ? ceilf(sc) : fl;
+    } else {
+      noise = u01(rbits[k]) - 0.5f;
+      r = rintf(sc - noise);
+    }
+    const float rq = (MODE == FC_DITHERED) ? (r + noise) : r;
+    const float dd = DIV == 1 ? sc - rq : xv - rq * cq.step;
+    dist = (!MASK || k < nvalid) ? fmaf(dd, dd, dist) : dist;
+    q[k] = r;
+    nz[k] = r != 0.0f;
+    nnz += (int32_t)__popcll(__ballot(nz[k]));
+  }
+  ChainCode r;
+#if FC_NZ_ADDC
+  {
+    const uint64_t b0 = __ballot(nz[0]), b1 = __ballot(nz[1]), b2 = __ballot(nz[2]);
+    uint64_t cj;
+    uint32_t m = nz[3] ? 1u : 0u;
+    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(m), "=s"(cj) : "v"(m), "s"(b2));
+    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(m), "=s"(cj) : "v"(m), "s"(b1));
+    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(m), "=s"(cj) : "v"(m), "s"(b0));
+    r.nzm = m;
+  }
+#else
+  r.nzm = (nz[0] ? 1u : 0u) | (nz[1] ? 2u : 0u) | (nz[2] ? 4u : 0u) | (nz[3] ? 8u : 0u);
+#endif
+  const float mabs = vmax3_abs(q[0], q[1], vmax3_abs(q[2], q[3], 0.0f));
+  const bool bad = !(mabs < 8192.0f);
+  r.acc = 0;
+  r.len = 0;
+  if (__ballot(!(mabs <= 7.0f)) == 0) {
+    // |q| <= 7 across the wave: two chained pair-table reads
+    const uint32_t a0 = __float_as_uint(fmaf(q[0], 4.0f, 12582912.0f));
+    const uint32_t b0 = __float_as_uint(fmaf(q[1], 64.0f, 12582912.0f));
+    const uint32_t e0 = *(const uint32_t*)((const char*)plut + ((a0 & 0x3Cu) | (b0 & 0x3C0u) | sst));
+    const uint32_t a1 = __float_as_uint(fmaf(q[2], 4.0f, 12582912.0f));
+    const uint32_t b1 = __float_as_uint(fmaf(q[3], 64.0f, 12582912.0f));
+    const uint32_t e1 =
+        *(const uint32_t*)((const char*)plut + ((a1 & 0x3Cu) | (b1 & 0x3C0u) | (e0 & kChainState)));
+    sst = e1 & kChainState;
+    const uint32_t l1 = e1 & 31u;
+    r.acc = ((uint64_t)(e0 >> 14) << l1) | (e1 >> 14);
+    r.len = (e0 & 31u) + l1;
+    r.pre = (e0 | e1) & kChainFlag;
+    r.lng = 0;  // |q| <= 7: at most 36 bits
+    return r;
+  } else {
+    // codes without the chunk's first run code, as quant_code_fast; the caller
+    // prepends it when the lane had a nonzero before the chunk
+    const uint32_t dv1 = nz[0] ? 1u : 0u;
+    const uint32_t dv2 = nz[1] ? 1u : (nz[0] ? 2u : 0u);
+    const uint32_t rl2 = nz[1] ? 1u : (nz[0] ? 3u : 0u);
+    const uint32_t dv3 = nz[2] ? 1u : (nz[1] ? 2u : (nz[0] ? 3u : 0u));
+    const uint32_t rl3 = nz[2] ? 1u : ((nz[1] || nz[0]) ? 3u : 0u);
+    const uint32_t dv[4] = {0u, dv1, dv2, dv3};
+    const uint32_t rl[4] = {0u, dv1, rl2, rl3};
+    const bool big = !(mabs <= 31.0f);
+    if (__ballot(big) == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t qb = __float_as_uint(fmaf(q[k], 4.0f, 12582912.0f)) & 0xFCu;
+        const uint32_t e = *(const uint32_t*)((const char*)clut + ((dv[k] << 8) | qb));
+        const uint32_t L = e >> 16;
+        r.acc = k == 0 ? (uint64_t)(e & 0xFFFFu) : ((r.acc << L) | (e & 0xFFFFu));
+        r.len += L;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t m = (uint32_t)fabsf(q[k]);
+        const uint32_t ml = 2u * ((__float_as_uint(q[k]) >> 23) & 0xFFu) - 253u;
+        const uint32_t t = 2u * dv[k] + (q[k] > 0.0f ? 1u : 0u);
+        uint32_t mk = nz[k] ? 0xFFFFFFFFu : 0u;
+        asm volatile("" : "+v"(mk));
+        const uint32_t code = ((t << ml) | m) & mk;
+        const uint32_t L = (rl[k] + ml + 1u) & mk;
+        r.acc = k == 0 ? (uint64_t)code : ((r.acc << L) | code);
+        r.len += L;
+      }
+    }
+    const uint32_t nzm = r.nzm;
+    r.pre = (nzm != 0u && sst != 0u) ? 1u : 0u;
+    // the state after the chunk: distance from its last nonzero to the next chunk
+    const uint32_t far = kChainFar << 10;
+    sst = nzm ? (4u - (31u - (uint32_t)__builtin_clz(nzm))) << 10 : (sst ? min(sst + (4u << 10), far) : 0u);
+  }
+  r.lng = (bad || r.len > 64u) ? 1u : 0u;
+  return r;
 }
 
 // Re-read and re-quantise one chunk (slow path: tiles with codes > 32 bits or
@@ -1778,12 +1967,17 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
 // half starts, so its round trip overlaps that half's work, and the LDS holds one
 // window of the super-tile's size instead of two.  Statuses are per super-tile
 // (slot t2 of the client's row); the decoder index stays per 1024-element tile.
+#ifndef FC_PAIR_CHAIN
+#define FC_PAIR_CHAIN 1  // k_encode2: the chained pair table (run state across the lane's chunks)
+#endif
 #ifndef FC_WIN2_WORDS
-#define FC_WIN2_WORDS (2 * FC_WIN_WORDS)
+// the chained table's 8 KiB come out of the windows: four 4-wave workgroups per CU
+#define FC_WIN2_WORDS (FC_PAIR_CHAIN ? 952 : 2 * FC_WIN_WORDS)
 #endif
 constexpr uint32_t kWin2Words = FC_WIN2_WORDS;
 // four-tile tickets while codes are expected within this many bits per element
-// (their window holds 32 * kWin2Words - kPre - 96 bits = ~8.4 bits per element)
+// (their window holds 32 * kWin2Words - kPre - 96 bits = ~7.4 bits per element with
+// the chained pair table, ~8.4 without)
 constexpr double kNt4Bits = 6.5;
 constexpr int kSTE = 2 * kTE;  // elements per super-tile
 
@@ -1819,10 +2013,13 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
   constexpr int STE = NT * kTE;  // elements per super-tile (ticket)
   __shared__ uint32_t wins[kEnc2Waves][kWin2Words + 3];  // + guard words
   __shared__ uint32_t clut[kCodeLut];
-  __shared__ uint32_t plut[kPairLut];
+  constexpr bool CHAIN = FC_PAIR_CHAIN && FC_PAIR_LUT && !INT_IN;
+  constexpr int kPL = CHAIN ? kChainLut : kPairLut;
+  __shared__ uint32_t plut[kPL];
   __shared__ __attribute__((aligned(16))) uint32_t stgs[kEnc2Waves][kTE];  // LDS-DMA staging of the next tile
   for (int i = threadIdx.x; i < kCodeLut; i += kEncThreads * kEnc2Waves) clut[i] = code_lut_entry((uint32_t)i);
-  for (int i = threadIdx.x; i < kPairLut; i += kEncThreads * kEnc2Waves) plut[i] = pair_lut_entry((uint32_t)i);
+  for (int i = threadIdx.x; i < kPL; i += kEncThreads * kEnc2Waves)
+    plut[i] = CHAIN ? pair_chain_entry((uint32_t)i) : pair_lut_entry((uint32_t)i);
   const int wave = (int)uniform(threadIdx.x >> 6);  // wave-uniform (the compiler cannot tell)
   const int lane = (int)(threadIdx.x & 63u);
   uint32_t* win = wins[wave];
@@ -1943,6 +2140,39 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       uint32_t clen[kChunks];
       const int32_t hrel = h * kTE + lrel;
       const uint32_t gbase = (uint32_t)(tile_base >> 2) + 4u * (uint32_t)lane + cq.gofs;  // Philox counter of chunk 0
+      if (CHAIN) {
+        // run state across the lane's chunks: only a far run (or a chunk off the
+        // pair table) needs its first run code prepended, from the lane's mask
+        uint32_t sst = 0, lmask = 0;
+#pragma unroll
+        for (int j = 0; j < kChunks; ++j) {
+          const uint32_t g = gbase + (uint32_t)j;
+          ChainCode cc;
+          if (MODE == FC_DITHERED && !full)
+            cc = quant_code_chain<MODE, DIV, PRE, true>(
+                cq, g, raw[j], dist, nnz, clut, plut, sst,
+                (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - lrel - 4 * j)));
+          else
+            cc = quant_code_chain<MODE, DIV, PRE>(cq, g, raw[j], dist, nnz, clut, plut, sst);
+          if (__ballot(cc.pre != 0u) != 0) {
+            if (cc.pre) {  // a nonzero before it in the lane: lmask != 0
+              const uint32_t d = 4u * (uint32_t)j + (uint32_t)__builtin_ctz(cc.nzm) - (31u - (uint32_t)__builtin_clz(lmask));
+              const uint32_t rl = 63u - 2u * (uint32_t)__builtin_clz(d);  // glen(d)
+              cc.lng |= (cc.len + rl > 64u) ? 1u : 0u;
+              cc.acc |= (uint64_t)d << (cc.len & 63u);
+              cc.len += rl;
+            }
+          }
+          lmask |= cc.nzm << (4 * j);
+          lng |= cc.lng;
+          cacc[j] = cc.acc;
+          clen[j] = cc.len;
+          llen += cc.len;
+          FC_CHUNK_BARRIER;
+        }
+        lfirst = lmask ? hrel + (int32_t)__builtin_ctz(lmask) : -1;
+        llast = lmask ? hrel + 31 - (int32_t)__builtin_clz(lmask) : -1;
+      } else
 #pragma unroll
       for (int j = 0; j < kChunks; ++j) {
         const int32_t rel0 = hrel + 4 * j;
@@ -1963,7 +2193,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           else
             cc = quant_code_fast<MODE, DIV, PRE, false, FC_PAIR_LUT>(cq, g, raw[j], rel0, dist, nnz, clut, 4, plut);
         }
-        chunk_prepend(cc, llast);  // no-op without an earlier nonzero in the lane
+        if (!(FC_ABL & 8192)) chunk_prepend(cc, llast);  // no-op without an earlier nonzero in the lane
         lfirst = lfirst < 0 ? cc.first : lfirst;
         llast = cc.last >= 0 ? cc.last : llast;
         lng |= cc.lng;

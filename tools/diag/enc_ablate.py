@@ -2,7 +2,8 @@
 
 LIBS="a.so b.so ..." C=1024 P=25000000 python tools/diag/enc_ablate.py
 Encode only (ablation builds write streams the decoder must not be fed); HIP
-events, median of REPS, stochastic and uniform modes, step 0.5.
+events, median of REPS, stochastic and uniform modes, step 0.5.  CAP: stream capacity
+in bytes per element (it is also the encoder's density hint).
 """
 import os
 import sys
@@ -23,7 +24,7 @@ for c in range(C):
   rows.append(torch.randn(P, generator=g, device=dev))
 ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
 seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
-batch = codec.EncodedBatch(P, C, [P + 1024] * C, dev)
+batch = codec.EncodedBatch(P, C, [int(P * float(os.environ.get("CAP", 1.0))) + 1024] * C, dev)  # CAP bytes/element (< 0.8: four-tile tickets)
 s = torch.cuda.current_stream()
 for path in os.environ["LIBS"].split():
   _lib._lib = None  # pylint: disable=protected-access
