@@ -1082,7 +1082,8 @@ __device__ __forceinline__ void chunk_prepend(ChunkCode& r, int32_t prev) {
 // Chained pair table (k_encode2, FC_PAIR_CHAIN): the run state crosses the
 // lane's chunks, so a chunk's first nonzero takes its run code from the table
 // like every other nonzero, and no per-chunk first / last nonzero or prepend is
-// computed.  Entry (s << 8) | ((qb & 15) << 4) | (qa & 15): s = distance from the
+// computed.  Entry (s << 8) | ((qa + 16 qb) & 255) -- one index for |qa|, |qb| <= 7,
+// formed by two FMAs on the rounded floats -- with s = distance from the
 // lane's last nonzero to qa, 1..6; 0 no nonzero yet in the lane (the lane's first
 // run code comes from the wave scan); 7 "far" (>= 7: a nonzero here is coded
 // without its run code and flagged, and the caller prepends the exact one).
@@ -1095,7 +1096,8 @@ constexpr uint32_t kChainFlag = 1u << 13;
 constexpr uint32_t kChainState = 7u << 10;
 __device__ __forceinline__ uint32_t pair_chain_entry(uint32_t i) {
   const uint32_t s = i >> 8;
-  const int32_t qa = ((int32_t)(i << 28)) >> 28, qb = ((int32_t)(i << 24)) >> 28;
+  const int32_t qa = ((int32_t)(i << 28)) >> 28;
+  const int32_t qb = ((int32_t)((((i & 255u) - (uint32_t)qa) & 255u) << 24)) >> 28;
   if (qa < -7 || qb < -7) return 0u;  // |q| = 8: never looked up
   uint32_t code = 0, len = 0, flag = 0;
   const int32_t qs[2] = {qa, qb};
@@ -1188,17 +1190,16 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
   r.len = 0;
   if (__ballot(!(mabs <= 7.0f)) == 0) {
     // |q| <= 7 across the wave: two chained pair-table reads
-    const uint32_t a0 = __float_as_uint(fmaf(q[0], 4.0f, 12582912.0f));
-    const uint32_t b0 = __float_as_uint(fmaf(q[1], 64.0f, 12582912.0f));
-    const uint32_t e0 = *(const uint32_t*)((const char*)plut + ((a0 & 0x3Cu) | (b0 & 0x3C0u) | sst));
-    const uint32_t a1 = __float_as_uint(fmaf(q[2], 4.0f, 12582912.0f));
-    const uint32_t b1 = __float_as_uint(fmaf(q[3], 64.0f, 12582912.0f));
-    const uint32_t e1 =
-        *(const uint32_t*)((const char*)plut + ((a1 & 0x3Cu) | (b1 & 0x3C0u) | (e0 & kChainState)));
+    // 1.5 * 2^23 + 4 qa + 64 qb is an exact float integer whose low 10 bits are
+    // 4 * ((qa + 16 qb) mod 256): the pair's byte offset in a state region
+    const uint32_t t0 = __float_as_uint(fmaf(q[1], 64.0f, fmaf(q[0], 4.0f, 12582912.0f)));
+    const uint32_t e0 = *(const uint32_t*)((const char*)plut + ((t0 & 0x3FCu) | sst));
+    const uint32_t t1 = __float_as_uint(fmaf(q[3], 64.0f, fmaf(q[2], 4.0f, 12582912.0f)));
+    const uint32_t e1 = *(const uint32_t*)((const char*)plut + ((t1 & 0x3FCu) | (e0 & kChainState)));
     sst = e1 & kChainState;
     const uint32_t l1 = e1 & 31u;
     r.acc = ((uint64_t)(e0 >> 14) << l1) | (e1 >> 14);
-    r.len = (e0 & 31u) + l1;
+    r.len = (e0 + e1) & 63u;  // bits 9:5 are zero: the two lengths add without interference
     r.pre = (e0 | e1) & kChainFlag;
     r.lng = 0;  // |q| <= 7: at most 36 bits
     return r;
