@@ -186,7 +186,7 @@ def auto_segments(nclients, P):
   if env:
     return max(1, int(env))
   C, P = int(nclients), int(P)
-  if C > 256 or P < (1 << 21):  # 512 x 25 M: two segments measured even (26.73 / 26.77 ms)
+  if C > 256 or P < (1 << 21):  # 512 x 25 M runs the super-tile encoder whole: 15.9 ms, two segments 17.7
     return 1
   k = 1024 // C
   while k > 1 and P // k < (1 << 18):

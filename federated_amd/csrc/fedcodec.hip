@@ -4029,17 +4029,21 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu0, kern2, kEncThreads * kEnc2Waves, 0) != hipSuccess ||
       per_cu0 < 1)
     per_cu0 = 1;
-  bool super = (int64_t)ncu * per_cu0 * kEnc2Waves <= 4LL * nclients && T >= 2;
-  if (const char* e = getenv("FEDCODEC_ENC2")) super = atoi(e) != 0;  // test knob
-  if (idxq) super = false;  // quarter-tile entries come from the one-tile kernel (few clients)
   // four tiles per ticket (FEDCODEC_ENC_NT=4): the per-ticket work (ticket, status,
   // look-back, reductions, store set-up) paid once per 4096 elements; the window
-  // (the same LDS) then holds about 8.4 bits per element before the exact path
+  // (the same LDS) then holds about 7.4 bits per element before the exact path
   // by the caller's largest stream capacity (host-known): codes expected within
   // kNt4Bits bits per element (+ slack) take four-tile tickets; denser ones, or an
   // unknown capacity, two (a window overflow sends the client to the exact path)
   int nt = (max_cap > 0 && 8.0 * (double)max_cap <= kNt4Bits * (double)P + 8.0 * 8192.0) ? 4 : 2;
   if (const char* e = getenv("FEDCODEC_ENC_NT")) nt = atoi(e) == 4 ? 4 : 2;  // test knob
+  // with four-tile tickets (and the chained pair table) from 512 clients on a full
+  // chip: 512 x 25 M stochastic 22.1 (k_encode) -> 15.9 ms, uniform 19.6 -> 15.3
+  // (profiles/r03/diag_enc512.txt); fewer clients are segmented (codec.auto_segments)
+  const int64_t rows_per_wave = nt == 4 ? 8 : 4;
+  bool super = (int64_t)ncu * per_cu0 * kEnc2Waves <= rows_per_wave * nclients && T >= 2;
+  if (const char* e = getenv("FEDCODEC_ENC2")) super = atoi(e) != 0;  // test knob
+  if (idxq) super = false;  // quarter-tile entries come from the one-tile kernel (few clients)
   if (super) {
     kern = nt == 4 ? kern4 : kern2;
     a.T2 = (int32_t)((T + nt - 1) / nt);

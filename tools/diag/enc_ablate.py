@@ -16,6 +16,7 @@ from federated_amd import _lib, codec  # noqa: E402
 P = int(os.environ.get("P", 25_000_000))
 C = int(os.environ.get("C", 1024))
 REPS = int(os.environ.get("REPS", 5))
+SEG = int(os.environ["SEGMENTS"]) if os.environ.get("SEGMENTS") else None  # None: codec.auto_segments
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev)
 rows = []
@@ -35,10 +36,11 @@ for path in os.environ["LIBS"].split():
     for it in range(REPS + 1):
       e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
       e0.record(s)
-      codec.quantize_encode(None, 0.5, seeds, mode, ptrs=ptrs, P=P, out=batch, stream=s)
+      codec.quantize_encode(None, 0.5, seeds, mode, ptrs=ptrs, P=P, out=batch, stream=s, segments=SEG)
       e1.record(s)
       torch.cuda.synchronize()
       if it:
         ts.append(e0.elapsed_time(e1))
     ts.sort()
-    print("%-34s mode=%d C=%d  encode %.3f ms" % (os.path.basename(path), mode, C, ts[len(ts) // 2]), flush=True)
+    print("%-34s mode=%d C=%d seg=%s enc2=%s  encode %.3f ms" % (os.path.basename(path), mode, C, SEG,
+          os.environ.get("FEDCODEC_ENC2", "auto"), ts[len(ts) // 2]), flush=True)
