@@ -1355,13 +1355,17 @@ constexpr uint32_t kPre = 96;
 // sparse clients) all sit at the same window position -- unconditional ORs made
 // an all-zero round 2.5x slower than a dense one (81 vs 32 ms at 1024 x 25 M;
 // skipping each word a code does not reach costs 2 % more on dense data).
+#ifndef FC_EMIT_BRANCH
+#define FC_EMIT_BRANCH 1  // empty codes skip their ORs by a branch (0: their zero ORs go to lane-spread words)
+#endif
 template <uint32_t W = kWinWords>
 __device__ __forceinline__ void emit64(uint32_t* win, uint64_t acc, uint32_t len, uint32_t wp) {
   const uint64_t X = acc << ((64u - len) & 63u);  // MSB-aligned (len 0: acc is 0)
   const uint32_t o = wp & 31u;
-  const uint32_t i0 = min(wp >> 5, W);
+  uint32_t i0 = min(wp >> 5, W);
   const uint32_t hi = (uint32_t)(X >> 32), lo = (uint32_t)X;
-  if (len) {
+  if (!FC_EMIT_BRANCH) i0 = len ? i0 : (uint32_t)__lane_id();  // OR of zeros: any word, one per lane
+  if (!FC_EMIT_BRANCH || len) {
     atomicOr(&win[i0], hi >> o);
     atomicOr(&win[i0 + 1], __builtin_amdgcn_alignbit(hi, lo, o));
     atomicOr(&win[i0 + 2], __builtin_amdgcn_alignbit(lo, 0u, o));
@@ -1373,8 +1377,9 @@ template <uint32_t W = kWinWords>
 __device__ __forceinline__ void emit32(uint32_t* win, uint32_t v, uint32_t len, uint32_t wp) {
   const uint32_t X = (uint32_t)((uint64_t)v << ((32u - len) & 63u));  // MSB-aligned (len 0: v is 0)
   const uint32_t o = wp & 31u;
-  const uint32_t i0 = min(wp >> 5, W);
-  if (len) {
+  uint32_t i0 = min(wp >> 5, W);
+  if (!FC_EMIT_BRANCH) i0 = len ? i0 : (uint32_t)__lane_id();
+  if (!FC_EMIT_BRANCH || len) {
     atomicOr(&win[i0], X >> o);
     atomicOr(&win[i0 + 1], __builtin_amdgcn_alignbit(X, 0u, o));
   }
@@ -2911,7 +2916,8 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 #pragma unroll
     for (int u = 0; u < (LONG ? kDecLongUnroll : 1); ++u) {  // LONG: codes (each after a refill) per iteration
     if (u > 0 && cons >= total) break;
-    if (idle && (LONG || (it & (kDecLong - 1)) == 0 || __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES)) {
+    if (idle && (LONG || (it & (kDecLong - 1)) == 0 ||
+                 (FC_DEC_LONG_LANES <= 64 && __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES))) {
       // right after a refill (>= 33 window bits): one code decoded arithmetically
       const uint32_t top = (uint32_t)(r.win >> 32);
       const uint32_t z1 = (uint32_t)__clz(top);
