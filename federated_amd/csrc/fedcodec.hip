@@ -2602,7 +2602,11 @@ __device__ __noinline__ CodeVal slow_code(const uint8_t* base, int64_t cap, uint
 #define FC_DEC_ABL 0  // decoder ablation bits (diagnostics only): 1 sums one bank per lane, 2 no sums, 8 eight clients' streams for all lanes
 #endif
 #ifndef FC_DEC_REPL
-#define FC_DEC_REPL 1  // accumulator copies per workgroup (1 or 2; A/B knob)
+#define FC_DEC_REPL 1  // accumulator copies per workgroup (1, 2 or 4; A/B knob)
+#endif
+#ifndef FC_DEC_QTR_REPL
+#define FC_DEC_QTR_REPL 2  // the same for quarter-tile segments (dense streams: lanes in step on one address;
+                           // config 2 decode 0.32 -> 0.28 ms wall, 4 copies even)
 #endif
 #ifndef FC_DEC_BATCH
 #define FC_DEC_BATCH 4
@@ -2784,6 +2788,31 @@ __device__ __forceinline__ uint32_t lut_entry(uint32_t i) {
   return used ? (e | (used << 26)) : 0u;
 }
 
+// Single-code table (dense streams, the LONG loop): the next 12 window bits ->
+// the structure of the one code they begin, whenever its run code, sign and
+// magnitude prefix (up to the magnitude's leading 1) fit in them -- the
+// magnitude's remaining bits are then at a known place in the window:
+//   [4:0] L (0: not resolvable here -- the arithmetic decode takes the code)
+//   [9:5] n = magnitude bits   [10] negative   [15:11] d (1..31)
+// so m = bits [32 - L, 32 - L + n) of the window's top word (one v_bfe_u32).
+// Codes of |v| < 1024 after a run d < 32 -- every code of an 8-bit-step stream.
+#ifndef FC_DEC_GEN
+#define FC_DEC_GEN 1  // the LONG loop (dense streams) reads the single-code table first (A/B knob)
+#endif
+__device__ __forceinline__ uint32_t gen_entry(uint32_t i) {
+  const uint32_t top = i << (32 - kLutBits);
+  const uint32_t z1 = (uint32_t)__clz(top);
+  if (z1 > 4) return 0u;
+  const uint32_t sa = 30u - 2u * z1;  // sign-bit position
+  const uint32_t rest = top << (32u - sa);
+  const uint32_t z2 = (uint32_t)__clz(rest);
+  if (2u * z1 + 3u + z2 > (uint32_t)kLutBits) return 0u;  // the magnitude's leading 1 is past the index bits
+  const uint32_t L = 2u * (z1 + z2) + 3u;
+  const uint32_t d = top >> (sa + 1u);
+  const uint32_t neg = ((top >> sa) & 1u) ? 0u : 1u;
+  return L | ((z2 + 1u) << 5) | (neg << 10) | (d << 11);
+}
+
 constexpr int kDecThreads = 256;
 // Tiles per lane segment (accumulator path), chosen per launch: two with 256
 // lanes per tile pair once there are >= kDecSpan2Clients clients (half the
@@ -2830,11 +2859,12 @@ __device__ __forceinline__ void acc_add_at(uint32_t a, int32_t v, int32_t* ptile
 // window bits in the next arithmetic slot (longer than 32 bits: slow_code, then
 // the reader restarts).  The window holds >= 33 valid bits when an iteration
 // starts.
-template <int PLANE, bool LONG = false, bool STEP3 = false>
+template <int PLANE, bool LONG = false, bool STEP3 = false, bool GEN = false>
 __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap, uint64_t b0,
                                                uint64_t b1, int32_t rel, uint32_t my_addr,
                                                const uint32_t* lut, int32_t* err, int32_t* ptile,
-                                               uint32_t hib, uint32_t span = kTE) {
+                                               uint32_t hib, uint32_t span = kTE,
+                                               const uint16_t* glut = nullptr) {
   SegReader r;
   const int32_t total = (int32_t)(b1 - b0);
   r.init(base, cap, b0, total);
@@ -2916,7 +2946,25 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 #pragma unroll
     for (int u = 0; u < (LONG ? kDecLongUnroll : 1); ++u) {  // LONG: codes (each after a refill) per iteration
     if (u > 0 && cons >= total) break;
-    if (idle && (LONG || (it & (kDecLong - 1)) == 0 ||
+    bool tdone = false;
+    if (GEN && LONG) {
+      // right after a refill (>= 33 window bits, every resolvable code <= 21): one
+      // code from the single-code table; the run is at most 31 elements, so the
+      // accumulator position is bounded by the segment-end check like the table steps'
+      const uint32_t top = (uint32_t)(r.win >> 32);
+      const uint32_t e = glut[top >> (32 - kLutBits)];
+      const uint32_t L = e & 31u;
+      if (L != 0u) {
+        const uint32_t m = __builtin_amdgcn_ubfe(top, 32u - L, e >> 5);
+        const int32_t s = __builtin_amdgcn_sbfe((int32_t)e, 10, 1);  // -1: negative
+        relb += (e >> 11) << 2;
+        acc_add_at<PLANE>(relb, (int32_t)(m ^ (uint32_t)s) - s, ptile, hib, err);
+        r.win <<= L;
+        cons += (int32_t)L;
+        tdone = true;
+      }
+    }
+    if (!tdone && idle && (LONG || (it & (kDecLong - 1)) == 0 ||
                  (FC_DEC_LONG_LANES <= 64 && __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES))) {
       // right after a refill (>= 33 window bits): one code decoded arithmetically
       const uint32_t top = (uint32_t)(r.win >> 32);
@@ -2998,6 +3046,10 @@ template <int PLANE, int SPAN_ = 1, bool QTR = false, bool VIRT = false>
 #endif
 __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR ? FC_DEC_QTR_WPE : FC_DEC_WPE))) void k_decode(DecodeArgs a) {
   __shared__ uint32_t lut[kLutSize];  // static: table reads fold its base into the offset
+  // the single-code table for dense streams: quarter-tile segments (few clients,
+  // where 8-bit steps occur); the other variants keep their LDS for occupancy
+  constexpr bool GEN = FC_DEC_GEN && QTR && !PLANE;
+  __shared__ uint16_t glut[GEN ? kLutSize : 1];
   extern __shared__ int32_t acc[];     // [units_per_wg][UE] sums
   // a lane's segment: SPAN consecutive units of one client (the accumulator path)
   constexpr int SPAN = PLANE ? 1 : SPAN_;
@@ -3006,13 +3058,17 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
   const int tid = threadIdx.x;
   const int units_per_wg = kDecThreads / a.lanes_per_tile * SPAN;
   for (int i = tid; i < kLutSize; i += kDecThreads) lut[i] = lut_entry((uint32_t)i);
+  if (GEN)
+    for (int i = tid; i < kLutSize; i += kDecThreads) glut[i] = (uint16_t)gen_entry((uint32_t)i);
   const int sub = tid / a.lanes_per_tile;
   const int l = tid - sub * a.lanes_per_tile;
-  // FC_DEC_REPL accumulator copies (lane parity picks one, the copies one bank apart):
+  // REPL accumulator copies (lane l picks copy l mod REPL, the copies one bank apart):
   // fewer same-bank atomics from lanes at the same tile position
+  constexpr int REPL = PLANE ? 1 : QTR ? FC_DEC_QTR_REPL : FC_DEC_REPL;
+  static_assert(REPL == 1 || REPL == 2 || REPL == 4, "accumulator copies: 1, 2 or 4");
   const int rstride = units_per_wg * UE + 1;  // words between copies
   const uint32_t my_addr =
-      PLANE ? 0u : (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * SPAN * UE + (FC_DEC_REPL > 1 ? (l & 1) * rstride : 0));
+      PLANE ? 0u : (uint32_t)(uintptr_t)(lds_iptr)(acc + sub * SPAN * UE + (REPL > 1 ? (l & (REPL - 1)) * rstride : 0));
   const int64_t e_end = min(a.P, (int64_t)a.t_end * kTE);  // elements this launch writes
   const int64_t u_begin = (int64_t)a.t_begin * UPT;
   const int64_t u_end = (e_end + UE - 1) / UE;  // units holding elements of the range
@@ -3021,7 +3077,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
   for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int64_t u0 = u_begin + grp * units_per_wg;
     if (!PLANE) {
-      for (int i = tid; i < (FC_DEC_REPL > 1 ? 2 * rstride : units_per_wg * UE); i += kDecThreads) acc[i] = 0;
+      for (int i = tid; i < (REPL > 1 ? REPL * rstride : units_per_wg * UE); i += kDecThreads) acc[i] = 0;
       __syncthreads();
     }
     const int64_t u = u0 + sub * SPAN;
@@ -3090,8 +3146,8 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
         const uint32_t hib = PLANE ? 4u * (uint32_t)min<int64_t>(kTE, a.P - unit_base) : 0u;
         // a wave whose segments are all long-code streams skips the table steps
         if (kDecLongBits > 0 && __ballot(bend - bstart < (uint64_t)kDecLongBits * span) == 0)
-          decode_segment<PLANE, true>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err, ptile, hib,
-                                      span);
+          decode_segment<PLANE, true, false, GEN>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err,
+                                                  ptile, hib, span, glut);
         else if (kDecStep3Bits16 > 0 && __ballot(bend - bstart >= (uint64_t)kDecStep3Bits16 * (span / 16)) == 0)
           decode_segment<PLANE, false, true>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err, ptile,
                                              hib, span);
@@ -3106,7 +3162,8 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
       const int64_t e = u0 * UE + i;
       if (e >= e_end) break;
       int32_t v = acc[i];
-      if (FC_DEC_REPL > 1) v = (int32_t)((uint32_t)v + (uint32_t)acc[i + rstride]);
+#pragma unroll
+      for (int k = 1; k < REPL; ++k) v = (int32_t)((uint32_t)v + (uint32_t)acc[i + k * rstride]);
       if (a.sum_in) v = (int32_t)((uint32_t)v + (uint32_t)a.sum_in[e]);
       if (a.sum_out) a.sum_out[e] = v;
       if (a.out) {
@@ -4618,7 +4675,8 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
                              : span == 2 ? k_decode<0, 2> : k_decode<0, 1>;
   const int ue = qtr ? kTE / 4 : kTE;  // elements per unit
   const int tpw = kDecThreads / lpt * span;  // units per workgroup
-  const size_t lds = plane ? 0 : (size_t)(FC_DEC_REPL > 1 ? 2 * (tpw * ue + 1) : tpw * ue) * sizeof(int32_t);
+  const int repl = qtr ? FC_DEC_QTR_REPL : FC_DEC_REPL;
+  const size_t lds = plane ? 0 : (size_t)(repl > 1 ? repl * (tpw * ue + 1) : tpw * ue) * sizeof(int32_t);
   // (+ the static kLutSize-word table)
   int dev = 0, ncu = 256, per_cu = 0;
   (void)hipGetDevice(&dev);

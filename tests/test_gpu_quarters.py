@@ -167,3 +167,46 @@ def test_quarter_decode_tile_ranges(gpu):
     assert (part[hi:].cpu().numpy() == 999).all()
   np.testing.assert_array_equal(pout.cpu().numpy(), fout.cpu().numpy())
   assert int(err.item()) == 0
+
+
+@pytest.mark.parametrize("inject", ["runs", "big", "huge", "all"])
+def test_dense_single_code_table_with_unresolvable_codes(gpu, inject):
+  """Dense streams (8-bit steps: every wave of quarter segments takes the LONG
+  loop, which reads the single-code table first) with codes the 12-bit table
+  cannot resolve mixed in: runs of 32+ zeros (the run code's prefix is too long),
+  |q| >= 1024 (the magnitude's leading 1 is past the index bits), |q| ~ 2^17 (codes
+  past 32 bits: slow_code and a reader restart), both signs, at unit starts and
+  ends.  Codes byte-identical to the oracle, the int32 sum exact."""
+  rng = np.random.default_rng(7 + len(inject))
+  P, C, step = 40_000, 6, 1.0 / 127
+  xs = []
+  for c in range(C):
+    x = (rng.standard_normal(P) * 0.25).astype(np.float32)
+    if inject in ("runs", "all"):
+      for s in rng.choice(P - 200, 40, replace=False):
+        x[s:s + int(rng.integers(32, 140))] = 0.0
+      x[256:256 + 33] = 0.0   # a run from a unit start
+      x[1024 - 40:1024] = 0.0  # a run up to a tile end
+    if inject in ("big", "all"):
+      pos = rng.choice(P, 60, replace=False)
+      x[pos] = (rng.integers(1024, 6000, pos.size) * rng.choice([-1, 1], pos.size) * step).astype(np.float32)
+      x[255] = np.float32(-2047 * step)
+      x[512] = np.float32(4095 * step)
+    if inject in ("huge", "all"):
+      pos = rng.choice(P, 8, replace=False)
+      x[pos] = (rng.integers(1 << 16, 1 << 18, pos.size) * rng.choice([-1, 1], pos.size) * step).astype(np.float32)
+    xs.append(x)
+  seeds = np.array([[90 + c, 5 * c + 1] for c in range(C)], np.int64)
+  rows = [torch.from_numpy(x).to(gpu) for x in xs]
+  b = codec.quantize_encode(rows, step, torch.from_numpy(seeds), _lib.STOCHASTIC,
+                            caps=[codec.worst_case_capacity(P)] * C, quarters=True)
+  assert b.quarters
+  qs = [oq.stochastic_quantize(xs[c], np.float32(step), tuple(seeds[c])) for c in range(C)]
+  for c in range(C):
+    code, nbits = ocodec.run_length_gamma_encode(qs[c])
+    assert b.client_code(c) == code and int(b.bits()[c]) == nbits
+  assert float(np.mean(b.bits().astype(np.float64))) / P >= 8.0  # dense: mostly LONG-loop waves
+  s, _, err = codec.decode_accumulate(b)
+  assert int(err.item()) == 0
+  np.testing.assert_array_equal(s.cpu().numpy(),
+                                np.sum(np.stack(qs).astype(np.int64), axis=0).astype(np.int32))
