@@ -24,6 +24,7 @@ SIGNATURES = {
     "fc_last_error": (ctypes.c_char_p, []),
     "fc_version": (ctypes.c_char_p, []),
     "fc_num_tiles": (_I64, [_I64]),
+    "fc_decode_tables": (_I32, [_P, _P, _I32]),
     "fc_encode_workspace_bytes": (_I64, [_I32, _I64]),
     "fc_quantize": (_INT, [_P, _I64, _F32, _I64, _I64, _INT, _P, _P, _P]),
     "fc_quantize_encode": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P,

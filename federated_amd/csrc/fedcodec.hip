@@ -4745,6 +4745,13 @@ int fc_debug_stamps(unsigned long long* host8, int reset) {
 }
 #endif
 int64_t fc_num_tiles(int64_t P) { return P <= 0 ? 0 : tiles_for(P); }
+int32_t fc_decode_tables(uint32_t* lut, uint16_t* glut, int32_t n) {
+  static constexpr DecTabs kHostTabs = make_dec_tabs();  // the same constant expression as g_dec_tabs
+  if (n < kLutSize || !lut || !glut) return fail(-1, "table buffers must hold 4096 entries");
+  std::memcpy(lut, kHostTabs.lut, sizeof(kHostTabs.lut));
+  std::memcpy(glut, kHostTabs.glut, sizeof(kHostTabs.glut));
+  return kLutSize;
+}
 int64_t fc_encode_workspace_bytes(int32_t nclients, int64_t P) {
   if (nclients <= 0 || P <= 0) return 256;
   return enc_workspace_bytes(nclients, P);

@@ -79,6 +79,13 @@ const char* fc_version(void);
 /* Number of encoder tiles for P elements: ceil(P / FC_TILE_ELEMS). */
 int64_t fc_num_tiles(int64_t P);
 
+/* Host copy of the decoder's compile-time tables (diagnostics and CPU tests; no
+ * GPU call): lut[i] = the up-to-two codes the 12 window bits i begin, glut[i] =
+ * the structure of the one code they begin (k_decode's layouts; the decode of
+ * tfc.run_length_gamma_decode, elias_gamma_encode.py:71-72).  n = entries the
+ * buffers hold; returns the table size (4096), or -1 when n is smaller. */
+int32_t fc_decode_tables(uint32_t* lut, uint16_t* glut, int32_t n);
+
 /* Device workspace bytes fc_quantize_encode / fc_rlgamma_encode need for a batch
  * of `nclients` clients of P elements each.  16-byte aligned pointer required. */
 int64_t fc_encode_workspace_bytes(int32_t nclients, int64_t P);
