@@ -149,6 +149,14 @@ def setup_dist(args):
   return rank, world
 
 
+def rccl_version():
+  """RCCL's version as torch reports it (torch.cuda.nccl on ROCm), or None."""
+  try:
+    return ".".join(str(v) for v in torch.cuda.nccl.version())
+  except Exception:  # pylint: disable=broad-except
+    return None
+
+
 def cpu_baseline(args):
   """Oracle "port" of the reference TF-CPU path on a bounded sample (rank 0, N=1).
 
@@ -236,11 +244,22 @@ def roofline(kernel, alg_bytes, launch_ms, workload):
           "alg_bytes_per_launch": alg_bytes, "launch_ms": round(launch_ms, 3)}
 
 
+PROBE_SEED_OFFSET = 7919
+
+
+def probe_seeds(seeds):
+  """The untimed probe round's seeds: other Philox streams than the timed round's."""
+  return seeds + PROBE_SEED_OFFSET
+
+
 def sized_batch(P, C, dev, encode, cap_per_elem=0.0):
   """The round's EncodedBatch with capacities as the factory sizes them: an
-  untimed probe encode (1 byte per element), then codec.CapacityHint (largest
+  untimed probe round (1 byte per element), then codec.CapacityHint (largest
   client code + 1/8 + 4 KiB) -- what QuantizeEncodeFactory uses from its second
-  round on.  cap_per_elem > 0: that fixed capacity instead."""
+  round on.  The probe encodes with other seeds (``probe_seeds``) than the timed
+  round, as the factory only knows the previous round's sizes (uniform rounding
+  draws no stream: there the probe's codes equal the timed ones).
+  cap_per_elem > 0: that fixed capacity instead."""
   if cap_per_elem > 0:
     return codec.EncodedBatch(P, C, [codec._round_up(int(P * cap_per_elem) + 256, 64)] * C, dev)  # pylint: disable=protected-access
   probe = codec.EncodedBatch(P, C, [codec._round_up(P + 256, 64)] * C, dev)  # pylint: disable=protected-access
@@ -266,7 +285,7 @@ def codec_round(name, rows, ptrs, P, step, mode, steps, warmup, stream, workload
   C = len(rows)
   dev = rows[0].device
   seeds = torch.tensor([[500 + c, 500 + c] for c in range(C)], dtype=torch.int64, device=dev)
-  batch = sized_batch(P, C, dev, lambda b: codec.quantize_encode(None, step, seeds, mode, ptrs=ptrs, P=P, out=b,
+  batch = sized_batch(P, C, dev, lambda b: codec.quantize_encode(None, step, probe_seeds(seeds), mode, ptrs=ptrs, P=P, out=b,
                                                                   stream=stream))
   out = torch.empty(P, dtype=torch.float32, device=dev)
   err = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -334,7 +353,7 @@ def w_trainer_round(rows, ptrs, P, steps, warmup, stream):
     s0 = np.where(keep, clip * np.minimum(inv, np.float32(1.0) / clip), np.float32(0.0)).astype(np.float32)
     pre = torch.from_numpy(np.stack([s0, w.numpy()], 1).astype(np.float32)).to(dev, non_blocking=True)
     if batch is None:
-      batch = sized_batch(P, C, dev, lambda b: codec.quantize_encode(None, step, seeds, _lib.UNIFORM, ptrs=ptrs, P=P,
+      batch = sized_batch(P, C, dev, lambda b: codec.quantize_encode(None, step, probe_seeds(seeds), _lib.UNIFORM, ptrs=ptrs, P=P,
                                                                       out=b, stream=stream, prescale=pre))
     t.phase("k_encode", lambda: codec.quantize_encode(None, step, seeds, _lib.UNIFORM, ptrs=ptrs, P=P, out=batch,
                                                       stream=stream, prescale=pre))
@@ -502,6 +521,7 @@ def onebit_sharded(args, rank, world, dev, stream):
         "config": {"workload": "config 5: %d clients x %d fp32 deltas, one-bit SGD (threshold 0), client-order "
                                "float32 decode-sum + RCCL float32 all-reduce" % (C, P),
                    "clients_per_gpu": Cg, "world_size": world, "backend": dist.get_backend(),
+                   "rccl_version": rccl_version(),
                    "parallelism": "client-sharded dp%d + float32 all-reduce in %d slabs" % (world, len(bounds) - 1)},
         "roofline": roofline("k_mask_encode", enc_bytes, ms["k_mask_encode"], "none"),
     }
@@ -551,7 +571,7 @@ def main():
 
   base = 1000 + rank * Cg
   seeds = torch.tensor([[base + c, base + c] for c in range(Cg)], dtype=torch.int64, device=dev)
-  batch = sized_batch(P, Cg, dev, lambda b: codec.quantize_encode(None, args.step_size, seeds, mode, ptrs=ptrs, P=P,
+  batch = sized_batch(P, Cg, dev, lambda b: codec.quantize_encode(None, args.step_size, probe_seeds(seeds), mode, ptrs=ptrs, P=P,
                                                                    out=b, stream=stream), args.cap_bytes_per_elem)
   out = torch.empty(P, dtype=torch.float32, device=dev)
   isum = torch.empty(P, dtype=torch.int32, device=dev)
@@ -657,6 +677,9 @@ def main():
                                                                                  args.step_size),
                    "clients_per_gpu": Cg, "world_size": world,
                    "backend": dist.get_backend() if world > 1 else None,
+                   "rccl_version": rccl_version(),
+                   "stream_capacity": "CapacityHint from an untimed probe round with other seeds" if not
+                   args.cap_bytes_per_elem else "%g bytes per element" % args.cap_bytes_per_elem,
                    "parallelism": "client-sharded dp%d + RCCL int32 all-reduce"
                    % world if world > 1 else "1 GPU"},
         "roofline": rl,

@@ -42,6 +42,8 @@ SIGNATURES = {
     "fc_quantize_encode_segmented": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _I32, _I64, _P, _P, _P, _P,
                                             _P, _P, _P, _P, _P, _I64, _P]),
     "fc_decode_accumulate": (_INT, [_P, _P, _P, _P, _I32, _I64, _P, _P, _P, _F32, _P, _P, _P]),
+    "fc_index_workspace_bytes": (_I64, [_I32, _I64]),
+    "fc_build_index": (_INT, [_P, _P, _P, _I32, _I64, _I64, _P, _P, _P, _P, _P, _I64, _P]),
     "fc_decode_scaled_workspace_bytes": (_I64, [_I32, _I64]),
     "fc_decode_accumulate_scaled": (_INT, [_P, _P, _P, _P, _I32, _I64, _P, _P, _P, _P, _P, _I64, _P]),
     "fc_decode_accumulate_scaled_bounded": (_INT, [_P, _P, _P, _P, _I32, _I64, _P, _P, _P, _P, _I32, _P, _I64,

@@ -43,3 +43,31 @@ def torch_to_np(dtype):
 def finish(t, shape, host):
   t = t.reshape(shape)
   return t.cpu().numpy() if host else t
+
+
+def sharded_rows(value, shape, sharded, multi, group=None):
+  """Client rows of one rank's block for a sharded round.
+
+  Returns (rows, host, lo, base): ``lo`` is this rank's first global client index
+  and ``base`` one clock base for the whole round (distributed.round_preamble),
+  both None unless ``multi``.  Under ``multi`` a rank whose values are rejected
+  (shape) still joins the preamble's all-reduce, and then EVERY rank raises -- a
+  rank raising alone would leave the others blocked in the round's collectives.
+  """
+  from federated_amd import distributed  # pylint: disable=g-import-not-at-top
+  rows, host, bad = [], False, None
+  if not (sharded and len(value) == 0):
+    try:
+      rows, vshape, host = to_device_rows(value, torch.float32)
+      if vshape != tuple(shape):
+        raise ValueError("client value shape %s != %s" % (vshape, tuple(shape)))
+    except ValueError as e:
+      if not multi:
+        raise
+      bad = e
+  if not multi:
+    return rows, host, None, None
+  lo, _, any_bad, base = distributed.round_preamble(len(rows), bad is not None, group)
+  if any_bad:
+    raise bad if bad is not None else ValueError("client values rejected on another rank")
+  return rows, host, lo, base

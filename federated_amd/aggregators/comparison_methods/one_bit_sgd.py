@@ -7,8 +7,6 @@ masked means, distortion ``sum (x - decode)^2 / P`` and bitrate ``(P + 64) / P``
 (:87-112).  Masks are kept bit-packed in HBM (1 bit per element), which is the
 wire format the bitrate already assumes.
 """
-import torch
-
 from federated_amd import distributed
 from federated_amd import tff_compat as tc
 from federated_amd.aggregators import _values
@@ -34,14 +32,9 @@ class OneBitSGDFactory(tc.UnweightedAggregationFactory):
       (config 5's 8-GPU split, distributed.onebit_round) and the distortion mean
       is global.  The multi-rank float association differs from one process's
       client-order sum: compare with a tolerance."""
-      if sharded and len(value) == 0:
-        rows, host = [], False
-      else:
-        rows, vshape, host = _values.to_device_rows(value, torch.float32)
-        if vshape != shape:
-          raise ValueError("client value shape %s != %s" % (vshape, shape))
-      rnd = distributed.onebit_round(rows, self._threshold, group=group, P=P, slabs=slabs,
-                                     multi=bool(sharded) and distributed.is_multi(group))
+      multi = bool(sharded) and distributed.is_multi(group)
+      rows, host, _, _ = _values.sharded_rows(value, shape, sharded, multi, group)
+      rnd = distributed.onebit_round(rows, self._threshold, group=group, P=P, slabs=slabs, multi=multi)
       return tc.MeasuredProcessOutput(
           state=state,
           result=_values.finish(rnd.result, shape, host),

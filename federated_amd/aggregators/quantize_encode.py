@@ -42,10 +42,11 @@ _NORMS = {"mean_magnitude": _lib.NORM_MEAN_MAGNITUDE, "max_magnitude": _lib.NORM
           "dimensionless_norm": _lib.NORM_DIMENSIONLESS}
 
 
-def clock_seeds(n):
-  """``tf.cast(tf.stack([tf.timestamp()*1e6]*2), tf.int64)`` per client, made distinct."""
-  base = int(time.time() * 1e6)
-  return np.array([[base + i, base + i] for i in range(n)], dtype=np.int64)
+def clock_seeds(n, base=None):
+  """``tf.cast(tf.stack([tf.timestamp()*1e6]*2), tf.int64)`` per client, made distinct
+  (client i gets base + i; ``base`` defaults to this process's clock)."""
+  base = int(time.time() * 1e6) if base is None else int(base)
+  return np.array([[base + i, base + i] for i in range(n)], dtype=np.int64).reshape(n, 2)
 
 
 class QuantizeEncodeFactory(tc.UnweightedAggregationFactory):
@@ -120,16 +121,15 @@ class QuantizeEncodeFactory(tc.UnweightedAggregationFactory):
       the torch.distributed world; distributed.aggregate_round) and every rank
       returns the round's global result.  The state is replicated: every rank
       steps it the same way."""
-      if sharded and len(value) == 0:
-        rows, host = [], False
-      else:
-        rows, vshape, host = _values.to_device_rows(value, torch.float32)
-        if vshape != shape:
-          raise ValueError("client value shape %s != %s" % (vshape, shape))
+      multi = bool(sharded) and distributed.is_multi(group)
+      # multi: one small all-reduce before the round's collectives -- a rank-local
+      # error is raised on every rank, and clock seeds come from ONE base (rank 0's)
+      # offset by the global client index, so no two clients of the round share a stream
+      rows, host, lo, base = _values.sharded_rows(value, shape, sharded, multi, group)
       C = len(rows)
       step_size = F32(state["step_size"])
       if seeds is None:
-        seeds = clock_seeds(C)
+        seeds = clock_seeds(C) if base is None else clock_seeds(C, base=base + lo)
       seeds = torch.as_tensor(np.asarray(seeds, np.int64).reshape(C, 2)).cuda()
       if prescale is not None:  # fused TFF wrapper scales (builder.configure_aggregator)
         prescale = torch.as_tensor(np.asarray(prescale, np.float32).reshape(C, 2)).cuda()
@@ -142,7 +142,7 @@ class QuantizeEncodeFactory(tc.UnweightedAggregationFactory):
       # elias_gamma_encode.py:100-108)
       rnd = distributed.aggregate_round(rows, step_size, seeds, factory._mode, group=group, prescale=prescale,
                                         norms=norms, caps=cap_hint.caps(P, C), P=P,
-                                        multi=bool(sharded) and distributed.is_multi(group))
+                                        multi=multi)
       if rnd.batch is not None:
         cap_hint.update(rnd.batch)
       next_round = F32(state["round_num"] + F32(1.0))

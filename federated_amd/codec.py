@@ -118,6 +118,70 @@ class EncodedBatch:
     return bytes(self.stream[off:off + nb].cpu().numpy().tobytes())
 
 
+def from_codes(codes, P, device=None, quarters=None, stream=None):
+  """An EncodedBatch holding BARE run-length gamma codes -- byte strings as
+  ``tfc.run_length_gamma_encode`` returns them, the reference's whole client message
+  (elias_gamma_encode.py:97-109) -- with the decoder index rebuilt on the device
+  from the bytes alone (fc_build_index), ready for ``decode_accumulate``: the
+  server side of ``tfc.run_length_gamma_decode(code, shape)`` (:69-73).
+
+  ``codes``: a list of bytes-like objects, one per client.  ``quarters``: also
+  rebuild the quarter-tile index (None: ``quarter_index_wanted``).  Raises
+  ValueError on a malformed code (one that does not parse, holds more or fewer
+  than P elements, or has bytes after its end).  ``total_bits`` is each code's
+  exact bit length; the per-tile distortion / nonzero partials are not defined.
+  """
+  _lib.require_gpu()
+  if device is None:
+    device = torch.device("cuda", torch.cuda.current_device())
+  codes = [bytes(c) for c in codes]
+  C = len(codes)
+  if C == 0:
+    raise ValueError("no codes")
+  lens = np.array([len(c) for c in codes], np.int64)
+  out = EncodedBatch(P, C, [int(n) + 16 for n in lens], device)
+  host = np.zeros(out._stream.numel(), np.uint8)  # pylint: disable=protected-access
+  for c, code in enumerate(codes):
+    o = int(out.offs_host[c])
+    host[o:o + len(code)] = np.frombuffer(code, np.uint8)
+  out._stream.copy_(torch.from_numpy(host))  # pylint: disable=protected-access
+  index_codes(out, torch.from_numpy(lens).to(device), int(lens.max()), quarters=quarters, stream=stream)
+  return out
+
+
+def index_codes(batch, nbytes, max_bytes, quarters=None, stream=None, check=True):
+  """fc_build_index over a batch whose streams hold bare codes of ``nbytes`` (device
+  int64 [C]) bytes each (max_bytes >= every one): rebuilds batch.idx (and the
+  quarter index), batch.total_bits.  Returns the device err flag; ``check`` raises
+  ValueError (one host sync) when a code is malformed."""
+  device = batch.device
+  C, P = batch.nclients, batch.P
+  want_q = quarter_index_wanted(C) if quarters is None else bool(quarters)
+  need = int(_lib.load().fc_index_workspace_bytes(C, int(max_bytes)))
+  ws = torch.empty(_round_up(need, 256), dtype=torch.uint8, device=device)
+  err = torch.zeros(1, dtype=torch.int32, device=device)
+  _lib.call("fc_build_index", _lib.ptr(batch._stream), _lib.ptr(batch.stream_off), _lib.ptr(nbytes), C, P,  # pylint: disable=protected-access
+            int(max_bytes), _lib.ptr(batch._idx), _lib.ptr(batch.ensure_quarters() if want_q else None),  # pylint: disable=protected-access
+            _lib.ptr(batch.total_bits), _lib.ptr(err), _lib.ptr(ws), ws.numel(), _lib.stream_handle(stream))
+  batch.quarters = want_q
+  batch.seg = None
+  batch.overflow.zero_()
+  if check and int(err.item()):
+    raise ValueError("malformed run-length gamma code")
+  return err
+
+
+def decode_codes(codes, P, sum_in=None, want_sum=True, out=None, step=1.0, noise_sum=None):
+  """``tfc.run_length_gamma_decode`` of every bare code + the int32 client sum (the
+  reference's federated_aggregate accumulate / merge, elias_gamma_encode.py:63-88),
+  optionally dequantised: returns (sum int32 or None, out float32 or None)."""
+  batch = from_codes(codes, P)
+  s, o, err = decode_accumulate(batch, sum_in=sum_in, want_sum=want_sum, out=out, step=step, noise_sum=noise_sum)
+  if int(err.item()):
+    raise ValueError("malformed run-length gamma code")
+  return s, o
+
+
 def split_stitch_wanted():
   """Whether a segmented batch stitches on a second stream while the round decodes
   the unstitched segments (fc_decode_accumulate_segmented).  Off by default

@@ -3209,6 +3209,359 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
 }
 
 // ---------------------------------------------------------------------------
+// Decoder index from bare codes.  The reference decodes a client's message with
+// tfc.run_length_gamma_decode(code, shape) -- the byte string alone
+// (elias_gamma_encode.py:69-73, message at :97-109) -- so a server that receives
+// stock TFC strings has no encoder index.  fc_build_index rebuilds it (and the
+// quarter index) from the bytes, bit for bit what the encoder writes:
+//   entry u = stream bit where the first code whose nonzero lies at or after
+//   element G u starts | (1 + the last nonzero before it) << 36
+// (G = 1024, or 256 with the quarter index), entry T = the bit where the trailing
+// zero-run code starts (or the stream's end).
+//
+// A prefix code is parsed serially, so each lane parses its own kIdxChunkBits
+// of a client's code from a GUESSED start -- the chunk's first bit taken as a
+// code start -- and records where its parse leaves the chunk (the first code
+// start at or after the chunk's end) and the zero runs it summed.  Run-length
+// gamma parses resynchronise fast: from a random bit they reach a true code start
+// within 25 bits on average, 120 bits at the 99th percentile and 630 at most
+// (measured on the oracle's codes: 3.8-bit, 10.3-bit, 2.7-bit, 1-bit and 0.2-bit
+// streams), so the guessed parse almost always ends where the true one does.
+//   k_idx_spec   every lane: the guessed parse of its chunk (exit bit, sum of runs)
+//   k_idx_sync   lane j re-parses from lane j-1's exit and from its guessed start
+//                in lockstep until both reach one code start (a few codes), and
+//                corrects its run sum; no meeting inside the chunk: a full parse
+//   k_idx_fix    a wave per client walks the chunks in order and redoes (serially,
+//                rarely) any chunk whose true start differs from the one used
+//   k_idx_scan   a wave per client: exclusive sums of the runs = the last nonzero
+//                before each chunk's first code
+//   k_idx_emit   every lane: the true parse of its chunk, writing the entries of
+//                the units its codes enter; the chunk holding the end checks the
+//                trailing run, the bit count and the byte length
+//   k_idx_check  a client whose code never ended is malformed
+// ---------------------------------------------------------------------------
+constexpr int kIdxChunkBits = 4096;
+constexpr int64_t kIdxFail = -1;  // "the parse failed" (a guessed start, or past the stream's end)
+
+struct IdxArgs {
+  const uint8_t* stream_buf;
+  const int64_t* stream_off;
+  const int64_t* nbytes;  // [nclients]: each client's byte string length
+  int32_t nclients;
+  int64_t P;
+  int32_t T;
+  int64_t nchunks;  // chunk lanes per client
+  int64_t* x1;      // [C][nchunks]: guessed parse's exit bit (kIdxFail: failed)
+  int64_t* n1;      //               its sum of runs
+  int64_t* x2;      //               true exit bit
+  int64_t* n2;      //               true sum of runs, then (k_idx_scan) the last nonzero before the chunk
+  int32_t* ended;   // [nclients]
+  uint64_t* idx;
+  uint64_t* idxq;   // nullable
+  int64_t* total_bits;
+  int32_t* err;
+};
+
+// MSB-first reader of one client's code: a 64-bit window of nv valid bits (the
+// bits past the code's end read as zeros and are not counted).
+struct IdxReader {
+  const uint32_t* w;
+  int64_t nbits;
+  int64_t wpos;  // stream bit of the next word to load
+  uint64_t win;
+  int32_t nv;
+  int64_t pos;   // stream bit at the window's MSB
+  __device__ __forceinline__ void refill() {
+    if (nv <= 32 && wpos < nbits) {
+      uint32_t v = bswap32(w[wpos >> 5]);
+      const int64_t vb = nbits - wpos;
+      if (vb < 32) v &= ~0u << (32 - (int32_t)vb);
+      win |= (uint64_t)v << (32 - nv);
+      nv += vb < 32 ? (int32_t)vb : 32;
+      wpos += 32;
+    }
+  }
+  __device__ __forceinline__ void skip(uint32_t n) {
+    win = n < 64 ? win << n : 0ull;
+    nv -= (int32_t)n;
+    pos += n;
+  }
+  __device__ __forceinline__ void init(const uint32_t* w_, int64_t nbits_, int64_t p) {
+    w = w_;
+    nbits = nbits_;
+    pos = p;
+    win = 0;
+    nv = 0;
+    wpos = p & ~31LL;
+    refill();
+    const int32_t s = (int32_t)(p & 31);
+    win = s < 64 ? win << s : 0ull;
+    nv = max(nv - s, 0);
+    if (nv == 0) win = 0;
+    refill();
+  }
+};
+
+// Elias gamma value at the reader (advanced past it); 0 when malformed (more than
+// 31 leading zeros) or cut by the stream's end.
+__device__ __forceinline__ uint32_t idx_gamma(IdxReader& r) {
+  r.refill();  // > 32 valid bits unless the stream ends
+  const uint32_t z = r.win ? (uint32_t)__clzll(r.win) : 64u;
+  if (z > 31u || (int32_t)z >= r.nv) return 0u;
+  if ((int32_t)(2u * z + 1u) <= r.nv) {
+    const uint32_t v = (uint32_t)((r.win << z) >> (63u - z));
+    r.skip(2u * z + 1u);
+    return v;
+  }
+  r.skip(z);
+  r.refill();
+  if ((int32_t)z + 1 > r.nv) return 0u;
+  const uint32_t v = (uint32_t)(r.win >> (63u - z));
+  r.skip(z + 1u);
+  return v;
+}
+
+// One (run, sign, magnitude) code: returns the run (>= 1), 0 if it does not parse.
+__device__ __forceinline__ uint32_t idx_code(IdxReader& r) {
+  const uint32_t d = idx_gamma(r);
+  if (!d) return 0u;
+  r.refill();
+  if (r.nv < 1) return 0u;
+  r.skip(1);
+  return idx_gamma(r) ? d : 0u;
+}
+
+__device__ __forceinline__ const uint32_t* idx_words(const IdxArgs& a, int64_t c) {
+  return (const uint32_t*)(a.stream_buf + a.stream_off[c]);
+}
+
+__global__ __launch_bounds__(kThreads) void k_idx_spec(IdxArgs a) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (int64_t)a.nclients * a.nchunks) return;
+  const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
+  const int64_t nbits = 8 * a.nbytes[c];
+  const int64_t cb = j * kIdxChunkBits, ce = cb + kIdxChunkBits;
+  int64_t x = kIdxFail, n = 0;
+  if (cb < nbits) {
+    IdxReader r;
+    r.init(idx_words(a, c), nbits, cb);
+    for (;;) {
+      if (r.pos >= ce) {
+        x = r.pos;
+        break;
+      }
+      const uint32_t d = idx_code(r);
+      if (!d) break;
+      n += d;
+    }
+  }
+  a.x1[g] = x;
+  a.n1[g] = n;
+}
+
+// Chunk [cb, ce) from its true start s: the guessed parse A (from cb: exit x1, runs
+// n1) replayed beside the true parse B until both stand on one code start, whence
+// they coincide.  Returns the true exit and runs; `met` false when B left the chunk
+// (or failed) without meeting A.
+struct IdxLock {
+  int64_t x, n;
+};
+__device__ __noinline__ IdxLock idx_lockstep(const uint32_t* w, int64_t nbits, int64_t cb, int64_t ce, int64_t s,
+                                             int64_t x1, int64_t n1) {
+  IdxReader A, B;
+  A.init(w, nbits, cb);
+  B.init(w, nbits, s);
+  int64_t pa = cb, pb = s, na = 0, nb = 0;
+  bool adone = false;
+  for (;;) {
+    if (pa == pb) return {x1, n1 - na + nb};
+    if (pa < pb && !adone) {
+      if (pa >= ce) {
+        adone = true;  // A left the chunk at x1
+        continue;
+      }
+      const uint32_t d = idx_code(A);
+      if (!d) {
+        adone = true;  // A failed at pa (x1 = fail)
+      } else {
+        na += d;
+        pa = A.pos;
+      }
+      continue;
+    }
+    if (pb >= ce) return {pb, nb};
+    const uint32_t d = idx_code(B);
+    if (!d) return {kIdxFail, nb};
+    nb += d;
+    pb = B.pos;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_idx_sync(IdxArgs a) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (int64_t)a.nclients * a.nchunks) return;
+  const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
+  const int64_t nbits = 8 * a.nbytes[c];
+  const int64_t cb = j * kIdxChunkBits;
+  IdxLock r{kIdxFail, 0};
+  if (j == 0) {
+    r = {a.x1[g], a.n1[g]};  // chunk 0 starts at bit 0: its parse is the true one
+  } else if (cb < nbits) {
+    const int64_t s = a.x1[g - 1];
+    if (s != kIdxFail) r = idx_lockstep(idx_words(a, c), nbits, cb, cb + kIdxChunkBits, s, a.x1[g], a.n1[g]);
+  }
+  a.x2[g] = r.x;
+  a.n2[g] = r.n;
+}
+
+__device__ __forceinline__ int64_t rfl64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// One wave per client: chunk j's true start is chunk j-1's final true exit; k_idx_sync
+// used chunk j-1's guessed exit, so a chunk whose predecessor's exit changed is
+// redone from the right start (lane 0, in order: a redone exit can change the next).
+__global__ __launch_bounds__(64) void k_idx_fix(IdxArgs a) {
+  const int64_t c = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t nbits = 8 * a.nbytes[c];
+  const int64_t nch = min<int64_t>(a.nchunks, (nbits + kIdxChunkBits - 1) / kIdxChunkBits);
+  if (nch <= 1) return;
+  const int64_t* x1 = a.x1 + c * a.nchunks;
+  const int64_t* n1 = a.n1 + c * a.nchunks;
+  int64_t* x2 = a.x2 + c * a.nchunks;
+  int64_t* n2 = a.n2 + c * a.nchunks;
+  const uint32_t* w = idx_words(a, c);
+  int64_t carried = x2[0];  // the final true exit of chunk j0 - 1
+  int64_t j0 = 1;
+  while (j0 < nch) {
+    const int64_t j = j0 + lane;
+    bool mism = false;
+    if (j < nch) mism = (lane == 0 ? carried : x2[j - 1]) != x1[j - 1];
+    const uint64_t m = __ballot(mism);
+    if (m == 0) {
+      carried = x2[min<int64_t>(j0 + 63, nch - 1)];
+      j0 += 64;
+      continue;
+    }
+    const int k = __builtin_ctzll(m);
+    const int64_t jk = j0 + k;
+    const int64_t s = k == 0 ? carried : x2[jk - 1];
+    IdxLock r{kIdxFail, 0};
+    if (lane == 0 && s != kIdxFail) {
+      const int64_t cb = jk * kIdxChunkBits;
+      r = idx_lockstep(w, nbits, cb, cb + kIdxChunkBits, s, x1[jk], n1[jk]);
+    }
+    if (lane == 0) {
+      x2[jk] = r.x;
+      n2[jk] = r.n;
+    }
+    carried = rfl64(r.x);
+    j0 = jk + 1;
+  }
+}
+
+// One wave per client: n2[j] <- the last nonzero before chunk j's first code
+// (-1 + the runs of every code before it).
+__global__ __launch_bounds__(64) void k_idx_scan(IdxArgs a) {
+  const int64_t c = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t nbits = 8 * a.nbytes[c];
+  const int64_t nch = min<int64_t>(a.nchunks, (nbits + kIdxChunkBits - 1) / kIdxChunkBits);
+  int64_t* n2 = a.n2 + c * a.nchunks;
+  int64_t run = -1;
+  for (int64_t j0 = 0; j0 < nch; j0 += 64) {
+    const int64_t j = j0 + lane;
+    const int64_t v = j < nch ? n2[j] : 0;
+    int64_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (j < nch) n2[j] = run + incl - v;
+    run += __shfl(incl, 63, 64);
+  }
+}
+
+__device__ __forceinline__ void idx_put(const IdxArgs& a, int64_t c, int64_t u, uint64_t e) {
+  if (!a.idxq) {
+    a.idx[c * (a.T + 1) + u] = e;
+    return;
+  }
+  const int64_t t = u >> 2;
+  const int s = (int)(u & 3);
+  if (s == 0) a.idx[c * (a.T + 1) + t] = e;
+  else a.idxq[3 * (c * a.T + t) + s - 1] = e;
+}
+
+__global__ __launch_bounds__(kThreads) void k_idx_emit(IdxArgs a) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (int64_t)a.nclients * a.nchunks) return;
+  const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
+  const int64_t nbits = 8 * a.nbytes[c];
+  const int64_t cb = j * kIdxChunkBits, ce = cb + kIdxChunkBits;
+  if (cb >= nbits) return;  // (an empty code never ends: k_idx_check)
+  const int64_t s = j == 0 ? 0 : a.x2[g - 1];
+  if (s == kIdxFail) return;  // past the code's end
+  int64_t L = a.n2[g];        // the last nonzero before the chunk's first code
+  if (L >= a.P) return;       // (past the trailing run of a code with bytes after it)
+  const int gs = a.idxq ? 8 : 10;  // unit: quarter tile or tile
+  IdxReader r;
+  r.init(idx_words(a, c), nbits, s);
+  int64_t u = (L + ((int64_t)1 << gs)) >> gs;  // the first unit starting after L
+  int64_t bend = -1, total = -1;
+  bool bad = false;
+  for (;;) {
+    const int64_t p = r.pos;
+    if (p >= ce) break;  // the next chunk's lane continues
+    if (L == a.P - 1) {  // every element covered, no trailing run
+      bend = total = p;
+      break;
+    }
+    const uint32_t d = idx_gamma(r);
+    if (!d || L + (int64_t)d > a.P) {
+      bad = true;
+      break;
+    }
+    if (L + (int64_t)d == a.P) {  // the trailing zero run
+      bend = p;
+      total = r.pos;
+      break;
+    }
+    r.refill();
+    if (r.nv < 1 || (r.skip(1), !idx_gamma(r))) {
+      bad = true;
+      break;
+    }
+    const int64_t nz = L + d;
+    const uint64_t e = ((uint64_t)p & kMask36) | ((uint64_t)(L + 1) << 36);
+    for (; (u << gs) <= nz; ++u) idx_put(a, c, u, e);
+    L = nz;
+  }
+  if (bad) {
+    atomicOr(a.err, 1);
+  } else if (bend >= 0) {
+    const uint64_t e = ((uint64_t)bend & kMask36) | ((uint64_t)(L + 1) << 36);
+    const int64_t nu = a.idxq ? 4 * (int64_t)a.T : (int64_t)a.T;
+    for (; u < nu; ++u) idx_put(a, c, u, e);
+    a.idx[c * (a.T + 1) + a.T] = e;
+    a.total_bits[c] = total;
+    a.ended[c] = 1;
+    if ((total + 7) / 8 != a.nbytes[c]) atomicOr(a.err, 1);  // bytes after the code, or a short final byte
+  } else if (ce >= nbits) {
+    atomicOr(a.err, 1);  // the code ends before its elements do
+  }
+}
+
+__global__ void k_idx_check(IdxArgs a) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < a.nclients && !a.ended[c]) atomicOr(a.err, 1);
+}
+
+// ---------------------------------------------------------------------------
 // Elementwise kernels.
 // ---------------------------------------------------------------------------
 template <int MODE>
@@ -4531,10 +4884,16 @@ bool seg_layout(int32_t C, int64_t P, int32_t K, int64_t max_cap, SegLayout& L) 
   L.nseg = K + (L.rem_elems > 0 ? 1 : 0);
   const int64_t nmain = (int64_t)C * K, nrem = L.rem_elems > 0 ? C : 0;
   L.nv = nmain + nrem;
-  // a segment's code needs at most its share of the client's capacity, plus slack
-  // for the first run code and the per-segment trailing code
-  L.vcap_main = (max_cap * L.seg_elems / P + 8192 + 255) / 256 * 256;
-  L.vcap_rem = nrem ? (max_cap * L.rem_elems / P + 8192 + 255) / 256 * 256 : 0;
+  // a segment's staging holds the client's whole capacity (bounded by the
+  // segment's worst case, 65 bits per element): a client whose nonzeros sit in
+  // one segment (model deltas are uneven across layers) fits whenever its code
+  // fits its own capacity -- a proportional share would overflow that segment and
+  // re-encode the client.  Plus slack for the first run code and the trailing code.
+  auto seg_cap = [&](int64_t n) {
+    return (std::min(max_cap, (65 * n + 64) / 8 + 64) + 8192 + 255) / 256 * 256;
+  };
+  L.vcap_main = seg_cap(L.seg_elems);
+  L.vcap_rem = nrem ? seg_cap(L.rem_elems) : 0;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
     const int64_t r = o;
@@ -4728,6 +5087,59 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   return check_launch("k_decode");
 }
 
+// fc_build_index workspace: x1 | n1 | x2 | n2 (int64 [nclients][nchunks] each) | ended (int32 [nclients]).
+int64_t idx_nchunks(int64_t max_bytes) { return std::max<int64_t>(1, (8 * max_bytes + kIdxChunkBits - 1) / kIdxChunkBits); }
+int64_t idx_workspace_bytes(int32_t n, int64_t max_bytes) {
+  return 4 * 8 * (int64_t)n * idx_nchunks(max_bytes) + ((4 * (int64_t)n + 255) & ~255LL);
+}
+
+int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* nbytes, int32_t nclients,
+                int64_t P, int64_t max_bytes, uint64_t* idx, uint64_t* idxq, int64_t* total_bits, int32_t* err,
+                void* workspace, int64_t workspace_bytes, void* stream) {
+  if (nclients <= 0) return fail(-1, "nclients must be > 0");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
+  if (max_bytes < 0) return fail(-1, "max_bytes must be >= 0");
+  if (!stream_buf || !stream_off || !nbytes || !idx || !total_bits || !err) return fail(-1, "null required pointer");
+  if (!workspace || workspace_bytes < idx_workspace_bytes(nclients, max_bytes) || ((uintptr_t)workspace & 15))
+    return fail(-1, "index workspace too small or not 16-byte aligned");
+  IdxArgs a;
+  a.stream_buf = stream_buf;
+  a.stream_off = stream_off;
+  a.nbytes = nbytes;
+  a.nclients = nclients;
+  a.P = P;
+  a.T = (int32_t)tiles_for(P);
+  a.nchunks = idx_nchunks(max_bytes);
+  const int64_t lanes = (int64_t)nclients * a.nchunks;
+  int64_t* w = (int64_t*)workspace;
+  a.x1 = w;
+  a.n1 = w + lanes;
+  a.x2 = w + 2 * lanes;
+  a.n2 = w + 3 * lanes;
+  a.ended = (int32_t*)(w + 4 * lanes);
+  a.idx = idx;
+  a.idxq = idxq;
+  a.total_bits = total_bits;
+  a.err = err;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(err, 0, sizeof(int32_t), s) != hipSuccess ||
+      hipMemsetAsync(a.ended, 0, 4 * (size_t)nclients, s) != hipSuccess)
+    return fail(-10, "memset");
+  const dim3 lgrid((unsigned)((lanes + kThreads - 1) / kThreads));
+  hipLaunchKernelGGL(k_idx_spec, lgrid, dim3(kThreads), 0, s, a);
+  if (const int rc = check_launch("k_idx_spec")) return rc;
+  hipLaunchKernelGGL(k_idx_sync, lgrid, dim3(kThreads), 0, s, a);
+  if (const int rc = check_launch("k_idx_sync")) return rc;
+  hipLaunchKernelGGL(k_idx_fix, dim3(nclients), dim3(64), 0, s, a);
+  if (const int rc = check_launch("k_idx_fix")) return rc;
+  hipLaunchKernelGGL(k_idx_scan, dim3(nclients), dim3(64), 0, s, a);
+  if (const int rc = check_launch("k_idx_scan")) return rc;
+  hipLaunchKernelGGL(k_idx_emit, lgrid, dim3(kThreads), 0, s, a);
+  if (const int rc = check_launch("k_idx_emit")) return rc;
+  hipLaunchKernelGGL(k_idx_check, dim3((unsigned)((nclients + 255) / 256)), dim3(256), 0, s, a);
+  return check_launch("k_idx_check");
+}
+
 }  // namespace
 
 extern "C" {
@@ -4869,6 +5281,17 @@ int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P, uin
   return encode_common((const void* const*)qs, nclients, P, 1.0f, nullptr, nullptr, nullptr, FC_UNIFORM, true,
                        stream_buf, stream_off, stream_cap, idx, total_bits, nullptr, nullptr, overflow,
                        workspace, workspace_bytes, stream);
+}
+
+int64_t fc_index_workspace_bytes(int32_t nclients, int64_t max_bytes) {
+  return nclients > 0 && max_bytes >= 0 ? idx_workspace_bytes(nclients, max_bytes) : -1;
+}
+
+int fc_build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* nbytes, int32_t nclients,
+                   int64_t P, int64_t max_bytes, uint64_t* idx, uint64_t* idxq, int64_t* total_bits, int32_t* err,
+                   void* workspace, int64_t workspace_bytes, void* stream) {
+  return build_index(stream_buf, stream_off, nbytes, nclients, P, max_bytes, idx, idxq, total_bits, err, workspace,
+                     workspace_bytes, stream);
 }
 
 int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap,

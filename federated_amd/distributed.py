@@ -89,6 +89,28 @@ def global_means(local_sums, nclients_local, device, group=None):
   return (v[:-1] / n if n else np.zeros(len(v) - 1)), int(n)
 
 
+def round_preamble(nclients_local, bad=False, group=None, device=None):
+  """What every rank of a sharded round must agree on before its collectives: ONE
+  small all-reduce of [client count per rank..., any rank's local error, rank 0's
+  clock].  Returns (lo, total, any_bad, base): this rank's first global client
+  index, the round's client count, whether any rank flagged an error (every rank
+  then raises instead of blocking in a later collective) and one clock base for
+  the whole round (rank 0's ``tf.timestamp()*1e6``, quantize_encode.py:141-144)."""
+  import time  # pylint: disable=g-import-not-at-top
+  world = dist.get_world_size(group)
+  rank = dist.get_rank(group)
+  if device is None:
+    device = torch.device("cuda", torch.cuda.current_device())
+  v = torch.zeros(world + 2, dtype=torch.int64, device=device)
+  v[rank] = int(nclients_local)
+  v[world] = 1 if bad else 0
+  if rank == 0:
+    v[world + 1] = int(time.time() * 1e6)
+  dist.all_reduce(v, op=dist.ReduceOp.SUM, group=group)
+  v = v.cpu().numpy()
+  return int(v[:rank].sum()), int(v[:world].sum()), bool(v[world]), int(v[world + 1])
+
+
 RoundOutput = collections.namedtuple("RoundOutput", ["result", "batch", "measurements"])
 
 
@@ -157,7 +179,11 @@ def aggregate_round(local_rows, step, local_seeds, mode, group=None, prescale=No
     for w in works:
       w.wait()
     out = codec.dequantize(isum, dq, noise)
-  if int(err.item()):
+  # multi-rank: a malformed code is flagged through the measurement all-reduce
+  # below, so every rank raises (a rank raising alone would leave the others
+  # blocked in the next collective)
+  bad = bool(int(err.item()))
+  if bad and not multi:
     raise RuntimeError("malformed run-length gamma code")
   if batch is not None:
     distortion, sparsity, bits = client_measurements(batch, P)
@@ -170,9 +196,11 @@ def aggregate_round(local_rows, step, local_seeds, mode, group=None, prescale=No
         avg_distortion=F32(np.mean(distortion, dtype=np.float32)),
         avg_sparsity=F32(np.mean(sparsity, dtype=np.float32)))
   else:
-    (mbits, mdist, mspars), _ = global_means(
-        [bits.sum(), distortion.astype(np.float64).sum(), sparsity.astype(np.float64).sum()], len(rows),
-        device, group)
+    (mbits, mdist, mspars, nbad), _ = global_means(
+        [bits.sum(), distortion.astype(np.float64).sum(), sparsity.astype(np.float64).sum(), float(bad)],
+        len(rows), device, group)
+    if nbad > 0:  # (only a rank holding clients decodes, so the count is > 0 then)
+      raise RuntimeError("malformed run-length gamma code (on at least one rank)")
     meas = collections.OrderedDict(
         avg_bitrate=np.float64(mbits / np.float64(P)) if P else np.float64(0.0),
         avg_distortion=F32(mdist), avg_sparsity=F32(mspars))

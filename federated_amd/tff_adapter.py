@@ -12,16 +12,14 @@ compute for the HIP codec, called through ``tf.numpy_function``:
 * client ``quantize`` (quantize_encode.py:139-156) + ``tfc.run_length_gamma_encode``
   (elias_gamma_encode.py:98) -> one ``fc_quantize_encode`` launch for the client;
   the client step is ``normalize_fn(value) * step`` (quantize_encode.py:145; the
-  norm from ``fc_client_norms``);
-  WIRE CHANGE: the client's message is the pair ``(code, index)`` of two
-  ``tf.string``s instead of the reference's single ``tf.string`` code
-  (elias_gamma_encode.py:97-109): the TFC byte string, unchanged, plus the
-  encoder's decoder index (8 bytes per 1024 elements, 0.06 bit/element), which
-  travels beside the code the way QSGD's norm travels beside its code
-  (qsgd.py:79).  ``avg_bitrate`` counts the code bytes only, as the reference;
+  norm from ``fc_client_norms``).  The client's message is the reference's: ONE
+  ``tf.string``, the TFC byte string (elias_gamma_encode.py:97-109), so stock
+  reference clients and these interoperate in either direction;
 * server ``federated_aggregate`` accumulate (elias_gamma_encode.py:69-73) ->
-  ``fc_decode_accumulate`` of one client into the running int32 sum;
-  merge (:75-77) is an int32 add;
+  ``fc_build_index`` (the decoder index rebuilt on the device from the bare bytes,
+  as ``tfc.run_length_gamma_decode(code, shape)`` needs nothing else) +
+  ``fc_decode_accumulate`` of the client into the running int32 sum; merge
+  (:75-77) is an int32 add;
 * server ``dequantize`` (quantize_encode.py:169-171) -> ``fc_dequantize``.
 
 TFF's executor maps clients one at a time, so this path encodes batches of
@@ -44,7 +42,7 @@ def _tf():
 
 
 def _encode_one(x, step, seed, mode, norm_kind=None):
-  """numpy_function body: one client -> (code bytes, index bytes, distortion, sparsity, noise).
+  """numpy_function body: one client -> (code bytes, distortion, sparsity, noise).
 
   ``norm_kind``: the factory's normalisation (quantize_encode.py:145: the client
   step is ``normalize_fn(value) * step``), None for "constant"."""
@@ -58,7 +56,6 @@ def _encode_one(x, step, seed, mode, norm_kind=None):
   batch = codec.quantize_encode_checked([x], float(step), seeds, int(mode), norms=norms)
   dist, nnz = codec.finalize(batch)
   code = batch.client_code(0)
-  index = batch.idx.cpu().numpy().tobytes()
   size = np.float32(P)
   distortion = np.float32(dist.cpu().numpy()[0] / size)
   sparsity = np.float32((size - np.float32(nnz.cpu().numpy()[0])) / size)
@@ -66,19 +63,16 @@ def _encode_one(x, step, seed, mode, norm_kind=None):
     noise = codec.noise_sum(seeds, P, x.device).cpu().numpy()
   else:
     noise = np.zeros(P, np.float32)
-  return code, index, distortion, sparsity, noise
+  return code, distortion, sparsity, noise
 
 
-def _decode_accumulate_one(acc, code, index):
-  """numpy_function body: acc + decode(code) (int32, wrapping)."""
+def _decode_accumulate_one(acc, code):
+  """numpy_function body: acc + tfc.run_length_gamma_decode(code, shape) (int32,
+  wrapping) from the bare byte string: the index is rebuilt on the device."""
   import torch  # pylint: disable=g-import-not-at-top
   from federated_amd import codec  # pylint: disable=g-import-not-at-top
   acc = torch.from_numpy(np.ascontiguousarray(acc, np.int32).reshape(-1)).cuda()
-  P = acc.numel()
-  batch = codec.EncodedBatch(P, 1, [max(len(code) + 64, 64)], acc.device)
-  if len(code):
-    batch.stream[:len(code)].copy_(torch.frombuffer(bytearray(code), dtype=torch.uint8))
-  batch.idx.copy_(torch.from_numpy(np.frombuffer(index, np.int64).copy()))
+  batch = codec.from_codes([bytes(code)], acc.numel(), device=acc.device)  # ValueError if malformed
   s, _, err = codec.decode_accumulate(batch, sum_in=acc)
   if int(err.item()):
     raise ValueError("malformed run-length gamma code")
@@ -97,19 +91,18 @@ def quantize_encode_process(value_type, factory):
   @tff.tf_computation(value_type, tf.float32)
   def quantize(value, step_size):
     seed = tf.cast(tf.stack([tf.timestamp() * 1e6, tf.timestamp() * 1e6]), dtype=tf.int64)
-    code, index, distortion, sparsity, noise = tf.numpy_function(
+    code, distortion, sparsity, noise = tf.numpy_function(
         lambda x, s, sd: _encode_one(x, s, sd, mode, norm_kind), [value, step_size, seed],
-        [tf.string, tf.string, tf.float32, tf.float32, tf.float32])
-    return (code, index), tf.reshape(noise, shape), distortion, sparsity
+        [tf.string, tf.float32, tf.float32, tf.float32])
+    return tf.reshape(code, []), tf.reshape(noise, shape), distortion, sparsity
 
   @tff.tf_computation
   def zero():
     return tf.zeros(shape, tf.int32)
 
   @tff.tf_computation
-  def accumulate(acc, message):
-    code, index = message
-    out = tf.numpy_function(_decode_accumulate_one, [acc, code, index], tf.int32)
+  def accumulate(acc, code):
+    out = tf.numpy_function(_decode_accumulate_one, [acc, code], tf.int32)
     return tf.reshape(out, shape)
 
   @tff.tf_computation
@@ -122,7 +115,7 @@ def quantize_encode_process(value_type, factory):
 
   @tff.tf_computation
   def bitstring_length(message):
-    return tf.cast(8 * tf.strings.length(message[0]), tf.float64)
+    return tf.cast(8 * tf.strings.length(message), tf.float64)
 
   @tff.tf_computation(tff.TensorType(tf.int32, shape), tf.float32,
                       tff.TensorType(tf.float32, shape))

@@ -217,6 +217,28 @@ int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off,
                          int64_t P, const int32_t* sum_in, int32_t* sum_out, float* out,
                          float step, const float* noise_sum, int32_t* err, void* stream);
 
+/* Decoder index of BARE run-length gamma codes: the reference server decodes a
+ * client's message with tfc.run_length_gamma_decode(code, shape) -- the byte
+ * string alone (elias_gamma_encode.py:69-73; the client message is that single
+ * tf.string, :97-109) -- so codes from a stock TFC client come without the
+ * encoder's index.  fc_build_index rebuilds it on the device from the bytes:
+ * idx (and, when idxq != NULL, the quarter index of fc_quantize_encode_quarters)
+ * and total_bits, bit for bit what the encoder writes, after which
+ * fc_decode_accumulate(_tiles / _quarters) decode the batch as usual.
+ *   stream_off  device int64[nclients]: client c's code at stream_buf + stream_off[c]
+ *               (4-byte aligned; readable up to the next 16-byte boundary past its end)
+ *   nbytes      device int64[nclients]: each code's byte length (the tf.string's length)
+ *   max_bytes   host: >= every nbytes[c] (sizes the work; fc_index_workspace_bytes)
+ *   err         device int32[1]: cleared, then set nonzero on a malformed code (a code
+ *               that does not parse, holds more or fewer than P elements, or whose
+ *               byte length is not ceil(bits / 8))
+ * Each lane parses 4096 bits of a code from a guessed start; the parses
+ * resynchronise within a few codes and are stitched. */
+int64_t fc_index_workspace_bytes(int32_t nclients, int64_t max_bytes);
+int fc_build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* nbytes, int32_t nclients,
+                   int64_t P, int64_t max_bytes, uint64_t* idx, uint64_t* idxq, int64_t* total_bits, int32_t* err,
+                   void* workspace, int64_t workspace_bytes, void* stream);
+
 /* fc_decode_accumulate restricted to tiles [tile_begin, tile_end) of 1024
  * elements: only elements [1024 * tile_begin, min(P, 1024 * tile_end)) of
  * sum_out / out are written.  err is OR'ed into, not cleared (zero it before the

@@ -185,3 +185,30 @@ def test_two_rank_onebit_reduction_matches_single_process():
     assert total == C
     np.testing.assert_allclose(got, want, rtol=1e-6 * C, atol=1e-6 * C * float(np.max(np.abs(want))))
     np.testing.assert_allclose(m, meas["avg_distortion"], rtol=1e-6)
+
+
+def _preamble_worker(rank, world, port, counts, bad_rank, out):
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  out[rank] = distributed.round_preamble(counts[rank], rank == bad_rank, device=torch.device("cpu"))
+  dist.destroy_process_group()
+
+
+def test_round_preamble_global_offsets_one_clock_and_shared_errors():
+  """round_preamble (the sharded factories' first collective): each rank's first
+  global client index, one clock base for every rank (so clock seeds base + global
+  index never repeat across ranks), and a rank-local error seen by every rank."""
+  from federated_amd.aggregators import quantize_encode  # pylint: disable=g-import-not-at-top
+  counts = [3, 0, 4]
+  for bad_rank in (-1, 1):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_preamble_worker, args=(3, _free_port(), counts, bad_rank, out), nprocs=3, join=True)
+    res = [out[r] for r in range(3)]
+    assert [r[0] for r in res] == [0, 3, 3]
+    assert all(r[1] == 7 for r in res)
+    assert all(r[2] == (bad_rank >= 0) for r in res)
+    assert len({r[3] for r in res}) == 1 and res[0][3] > 0
+    seeds = np.concatenate([quantize_encode.clock_seeds(counts[r], base=res[r][3] + res[r][0]) for r in range(3)])
+    assert len(np.unique(seeds[:, 0])) == sum(counts)

@@ -173,3 +173,30 @@ def test_unstitched_decode_tile_ranges(gpu, span, monkeypatch, _stitch_mode):
   assert int(err.item()) == 0 and int(e1.item()) == 0
   np.testing.assert_array_equal(part.cpu().numpy(), want.cpu().numpy())
   _same(seg, one)
+
+
+def test_segmented_skewed_client_fits_hint_capacity(gpu):
+  """Clients whose nonzeros all sit in ONE segment (model deltas are uneven across
+  layers), with the capacities QuantizeEncodeFactory uses from its second round on
+  (codec.CapacityHint: the previous round's largest code + 1/8 + 4 KiB): every
+  segment's staging holds the client's whole code, so no client overflows (and none
+  is re-encoded); the result equals the one-piece encode."""
+  C, P = 4, 1 << 22
+  K = codec.auto_segments(C, P)
+  assert K >= 8
+  rng = np.random.default_rng(8)
+  xs = [np.zeros(P, np.float32) for _ in range(C)]
+  for c in range(C):
+    lo = (3 * c % K) * (P // K)
+    xs[c][lo:lo + P // K] = (rng.standard_normal(P // K) * 4).astype(np.float32)
+  rows = [torch.from_numpy(x).to(gpu) for x in xs]
+  worst = [codec.worst_case_capacity(P)] * C
+  prev = codec.quantize_encode(rows, 0.5, torch.tensor([[c, c] for c in range(C)], dtype=torch.int64),
+                               _lib.STOCHASTIC, caps=worst, segments=1)
+  hint = codec.CapacityHint()
+  hint.update(prev)
+  seeds = torch.tensor([[90 + c, 3 * c] for c in range(C)], dtype=torch.int64)
+  seg = codec.quantize_encode(rows, 0.5, seeds, _lib.STOCHASTIC, caps=hint.caps(P, C))
+  assert not len(codec.check_overflow(seg))
+  one = codec.quantize_encode(rows, 0.5, seeds, _lib.STOCHASTIC, caps=worst, segments=1)
+  _same(seg, one)
