@@ -12,7 +12,8 @@ LIB_PATH = os.environ.get("FEDCODEC_LIB") or os.path.join(_HERE, "libfedcodec.so
 UNIFORM, STOCHASTIC, DITHERED = 0, 1, 2
 NORM_MEAN_MAGNITUDE, NORM_MAX_MAGNITUDE, NORM_DIMENSIONLESS, NORM_L2, NORM_LINF, NORM_L2_LINF = 1, 2, 3, 4, 5, 6
 TILE_ELEMS = 1024
-MAX_ELEMS = (1 << 26) - 1
+MAX_ELEMS = (1 << 28) - 1  # FC_MAX_ELEMS: one client tensor
+MAX_ROW_ELEMS = (1 << 26) - 1  # FC_MAX_ROW_ELEMS: one encoder row (longer tensors are segmented)
 
 # (name, restype, argtypes); every symbol declared in include/fedcodec.h.
 _P = ctypes.c_void_p
@@ -56,6 +57,7 @@ SIGNATURES = {
     "fc_vote_lengths": (_INT, [_P, _I32, _I64, _P, _I32, _P, _INT, _P, _P, _P, _I64, _P]),
     "fc_dequantize": (_INT, [_P, _I64, _F32, _P, _P, _P]),
     "fc_copy": (_INT, [_P, _P, _I64, _P]),
+    "fc_quantize_floor": (_INT, [_P, _I32, _I64, _F32, _P, _INT, _P, _P, _P, _I64, _P]),
     "fc_noise_sum": (_INT, [_P, _I32, _I64, _P, _P]),
     "fc_client_norms": (_INT, [_P, _I32, _I64, _INT, _P, _P]),
     "fc_client_norms_scaled": (_INT, [_P, _I32, _I64, _INT, _P, _P, _P]),

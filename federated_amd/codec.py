@@ -238,24 +238,42 @@ class SegWorkspace:
 _SEG_WS = SegWorkspace()
 
 
+def min_segments(P):
+  """Fewest segments that keep every segment one encoder row (<= 2^26 - 1 elements,
+  the look-back status's position width): 1 up to that size; longer tensors (up to
+  2^28 - 1, the decoder index's) are always encoded segmented and stitched."""
+  P = int(P)
+  if P <= _lib.MAX_ROW_ELEMS:
+    return 1
+  if P > _lib.MAX_ELEMS:
+    raise ValueError("client tensors hold at most 2^28 - 1 elements (P = %d)" % P)
+  k = -(-P // (_lib.MAX_ROW_ELEMS - 2 * 2048))
+  while P // k // 2048 * 2048 > _lib.MAX_ROW_ELEMS:
+    k += 1
+  return k
+
+
 def auto_segments(nclients, P):
   """Segments per client for the segmented encoder (1: none).
 
   The super-tile encoder wants about a thousand rows in flight; a batch of at
   most 256 clients of >= 2^21 elements is cut into 1024 / C segments per
-  client (each >= 2^18 elements).  ``FEDCODEC_SEGMENTS`` overrides (1 = off).
+  client (each >= 2^18 elements).  A tensor longer than one encoder row (2^26 - 1
+  elements) always is (``min_segments``).  ``FEDCODEC_SEGMENTS`` overrides (1 =
+  off), never below ``min_segments``.
   """
   import os  # pylint: disable=g-import-not-at-top
+  kmin = min_segments(P)
   env = os.environ.get("FEDCODEC_SEGMENTS")
   if env:
-    return max(1, int(env))
+    return max(kmin, int(env))
   C, P = int(nclients), int(P)
   if C > 256 or P < (1 << 21):  # 512 x 25 M runs the super-tile encoder whole: 15.9 ms, two segments 17.7
-    return 1
+    return kmin
   k = 1024 // C
   while k > 1 and P // k < (1 << 18):
     k //= 2
-  return max(1, min(63, k))
+  return max(kmin, min(63, k))
 
 
 def quarter_index_wanted(nclients, nseg=1):
@@ -317,13 +335,15 @@ def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, p
   seeds = torch.as_tensor(seeds, dtype=torch.int64).reshape(C, 2).to(device)
   if out is None:
     out = EncodedBatch(P, C, caps if caps is not None else [default_capacity(P)] * C, device)
-  nseg = auto_segments(C, P) if segments is None else int(segments)
+  nseg = auto_segments(C, P) if segments is None else max(int(segments), min_segments(P))
   out.join(stream)  # a previous round's stitch into this batch has finished
   out.seg = None
   if nseg > 1:
     max_cap = int(out.caps_host.max())
     split = split_stitch_wanted()
     sws = out.seg_workspace(nseg, max_cap) if split else _SEG_WS.get(C, P, nseg, max_cap, device)
+    if sws is None and nseg > 1 and P > _lib.MAX_ROW_ELEMS:
+      raise ValueError("cannot segment %d elements into %d segments" % (P, nseg))
     if sws is not None:
       main = stream if stream is not None else torch.cuda.current_stream()
       side = _stitch_stream(device) if split else main

@@ -3331,41 +3331,192 @@ __device__ __forceinline__ uint32_t idx_code(IdxReader& r) {
   return idx_gamma(r) ? d : 0u;
 }
 
+struct IdxLock {
+  int64_t x, n;
+};
+
 __device__ __forceinline__ const uint32_t* idx_words(const IdxArgs& a, int64_t c) {
   return (const uint32_t*)(a.stream_buf + a.stream_off[c]);
 }
 
-__global__ __launch_bounds__(kThreads) void k_idx_spec(IdxArgs a) {
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= (int64_t)a.nclients * a.nchunks) return;
-  const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
+__device__ __forceinline__ void idx_put(const IdxArgs& a, int64_t c, int64_t u, uint64_t e) {
+  if (!a.idxq) {
+    a.idx[c * (a.T + 1) + u] = e;
+    return;
+  }
+  const int64_t t = u >> 2;
+  const int s = (int)(u & 3);
+  if (s == 0) a.idx[c * (a.T + 1) + t] = e;
+  else a.idxq[3 * (c * a.T + t) + s - 1] = e;
+}
+
+// Table-driven parse of one chunk's codes: every code starting in [start, stop),
+// `start` a (true or guessed) code start.  The decoder's table (up to two complete
+// codes per 12 window bits, their runs and length) takes the common codes; a code
+// the table does not hold (longer than 12 bits, or the step would cross `stop` or,
+// EMIT, the next unit boundary) is decoded from the window's top 32 bits, and a
+// code longer than 32 bits -- or one that does not parse (the trailing zero-run
+// code, a guessed start, a malformed code) -- by the IdxReader, after which the
+// window restarts.
+//   !EMIT: returns the exit (first code start >= stop, or kIdxFail) and the runs' sum.
+//   EMIT: L = the last nonzero before `start` (true start); writes the entries of
+//   the units (from unit u on) its codes enter and, at the code's end, the tail
+//   entries, total_bits and `ended` (IdxEnd); bad on a malformed code.
+struct IdxEnd {
+  int64_t bend, total;  // bend >= 0: the code ended in this chunk
+  bool bad;
+};
+template <bool EMIT>
+__device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const uint32_t* lut, int64_t start,
+                                             int64_t stop, int64_t L, IdxEnd* end) {
   const int64_t nbits = 8 * a.nbytes[c];
-  const int64_t cb = j * kIdxChunkBits, ce = cb + kIdxChunkBits;
-  int64_t x = kIdxFail, n = 0;
-  if (cb < nbits) {
-    IdxReader r;
-    r.init(idx_words(a, c), nbits, cb);
-    for (;;) {
-      if (r.pos >= ce) {
-        x = r.pos;
+  const uint8_t* base = a.stream_buf + a.stream_off[c];
+  const int64_t cap = (a.nbytes[c] + 15) & ~15LL;  // readable: the 16-byte block holding the end
+  const uint32_t* w = (const uint32_t*)base;
+  const int gs = a.idxq ? 8 : 10;                  // EMIT unit: quarter tile or tile
+  const int64_t nu = a.idxq ? 4 * (int64_t)a.T : (int64_t)a.T;
+  int64_t u = EMIT ? (L + ((int64_t)1 << gs)) >> gs : 0;  // the first unit starting after L
+  // fast steps while the runs they add stay below `room4` (4 x elements to the next
+  // unit boundary, or to P once every boundary is written: a code reaching element P
+  // is the end's business)
+  auto room_of = [&](int64_t Lc) -> int32_t {
+    if (!EMIT) return 1 << 30;
+    const int64_t nb = u < nu ? min<int64_t>(u << gs, a.P) : a.P;
+    return (int32_t)min<int64_t>(4 * (nb - Lc), 1 << 30);
+  };
+  int64_t nsum = 0;  // !EMIT: the runs' sum outside the table steps
+  int32_t acc4 = 0;  // the table steps' runs (x 4) since the last slow code
+  int32_t room4 = room_of(L);
+  const int32_t lim = (int32_t)(stop - start);
+  // bits of the code from `start` on: a table / window code must end inside them (so
+  // every path accepts exactly the codes the IdxReader does)
+  const int32_t avail = (int32_t)min<int64_t>(nbits - start, (int64_t)lim + 8192);
+  SegReader r;
+  auto restart = [&](int32_t cons) {
+    r.init(base, cap, (uint64_t)(start + cons), (int32_t)min<int64_t>(nbits - start - cons, lim - cons + 8192));
+    return cons + r.nwin;
+  };
+  int32_t cons = 0;
+  int32_t fill = restart(0);
+  uint32_t it = 0;
+  while (cons < lim) {
+    if ((++it & (kDecBatch - 1)) == 0) r.batch();
+    const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+    const uint32_t Ls = e >> 26;
+    const int32_t dd4 = (int32_t)((e & 0x7Fu) + ((e >> 7) & 0x7Fu));
+    if (Ls != 0u && cons + (int32_t)Ls <= lim && cons + (int32_t)Ls <= avail && acc4 + dd4 < room4) {
+      r.win <<= Ls;
+      cons += (int32_t)Ls;
+      acc4 += dd4;
+    } else {
+      // one code: from the window's top 32 bits if it fits there (>= 33 valid bits)
+      const int64_t p = start + cons;
+      if (EMIT) {
+        L += acc4 >> 2;
+        acc4 = 0;
+      }
+      const uint32_t top = (uint32_t)(r.win >> 32);
+      const uint32_t z1 = (uint32_t)__clz(top);
+      const uint32_t sa = 30u - 2u * z1;
+      const uint32_t rest = top << (32u - sa);
+      const uint32_t z2 = (uint32_t)__clz(rest);
+      const uint32_t Lw = 2u * (z1 + z2) + 3u;
+      uint32_t d = top >> (sa + 1u);
+      bool took = false;
+      if (EMIT && L == a.P - 1) {  // every element covered: the code ends here, no trailing run
+        end->bend = end->total = p;
         break;
       }
-      const uint32_t d = idx_code(r);
-      if (!d) break;
-      n += d;
+      if (z1 <= 15u && z2 <= 15u && Lw <= 32u && cons + (int32_t)Lw <= avail && (!EMIT || L + (int64_t)d < a.P)) {
+        r.win <<= Lw;
+        cons += (int32_t)Lw;
+        took = true;
+      } else {
+        IdxReader ir;
+        ir.init(w, nbits, p);
+        d = idx_gamma(ir);
+        if (EMIT) {
+          if (!d || L + (int64_t)d > a.P) {
+            end->bad = true;
+            break;
+          }
+          if (L + (int64_t)d == a.P) {  // the trailing zero run
+            end->bend = p;
+            end->total = ir.pos;
+            break;
+          }
+        }
+        bool ok = d != 0u;
+        if (ok) {
+          ir.refill();
+          ok = ir.nv >= 1;
+          if (ok) {
+            ir.skip(1);
+            ok = idx_gamma(ir) != 0u;
+          }
+        }
+        if (!ok) {
+          if (EMIT) end->bad = true;
+          return {kIdxFail, nsum};
+        }
+        cons = (int32_t)(ir.pos - start);
+        fill = restart(cons);
+      }
+      if (EMIT) {
+        const int64_t nz = L + (int64_t)d;
+        const uint64_t en = ((uint64_t)p & kMask36) | ((uint64_t)(L + 1) << 36);
+        for (; u < nu && (u << gs) <= nz; ++u) idx_put(a, c, u, en);
+        L = nz;
+        room4 = room_of(L);
+      } else {
+        nsum += d;
+      }
+      if (!took) continue;  // the window restarted full
+    }
+    if (fill - cons <= 32) {  // (the blocks are zero past the code's end)
+      const uint32_t wd = r.pop32();
+      r.win |= (uint64_t)wd << (32 - (fill - cons));
+      fill += 32;
     }
   }
-  a.x1[g] = x;
-  a.n1[g] = n;
+  if (EMIT) {
+    L += acc4 >> 2;
+    if (!end->bad && end->bend >= 0) {
+      const uint64_t en = ((uint64_t)end->bend & kMask36) | ((uint64_t)(L + 1) << 36);
+      for (; u < nu; ++u) idx_put(a, c, u, en);
+      a.idx[c * (a.T + 1) + a.T] = en;
+      a.total_bits[c] = end->total;
+      a.ended[c] = 1;
+    }
+    return {start + cons, L};
+  }
+  return {start + cons, nsum + (acc4 >> 2)};
+}
+
+// The decode table in LDS for a workgroup of chunk lanes (persistent grids).
+__device__ __forceinline__ void idx_load_lut(uint32_t* lut) {
+  for (int i = threadIdx.x; i < kLutSize / 4; i += blockDim.x) ((uint4*)lut)[i] = ((const uint4*)g_dec_tabs.lut)[i];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kThreads) void k_idx_spec(IdxArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t lut[kLutSize];
+  idx_load_lut(lut);
+  const int64_t lanes = (int64_t)a.nclients * a.nchunks;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < lanes; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
+    const int64_t cb = j * kIdxChunkBits;
+    IdxLock r{kIdxFail, 0};
+    if (cb < 8 * a.nbytes[c]) r = idx_parse<false>(a, c, lut, cb, cb + kIdxChunkBits, 0, nullptr);
+    a.x1[g] = r.x;
+    a.n1[g] = r.n;
+  }
 }
 
 // Chunk [cb, ce) from its true start s: the guessed parse A (from cb: exit x1, runs
 // n1) replayed beside the true parse B until both stand on one code start, whence
 // they coincide.  Returns the true exit and runs; `met` false when B left the chunk
 // (or failed) without meeting A.
-struct IdxLock {
-  int64_t x, n;
-};
 __device__ __noinline__ IdxLock idx_lockstep(const uint32_t* w, int64_t nbits, int64_t cb, int64_t ce, int64_t s,
                                              int64_t x1, int64_t n1) {
   IdxReader A, B;
@@ -3486,73 +3637,28 @@ __global__ __launch_bounds__(64) void k_idx_scan(IdxArgs a) {
   }
 }
 
-__device__ __forceinline__ void idx_put(const IdxArgs& a, int64_t c, int64_t u, uint64_t e) {
-  if (!a.idxq) {
-    a.idx[c * (a.T + 1) + u] = e;
-    return;
-  }
-  const int64_t t = u >> 2;
-  const int s = (int)(u & 3);
-  if (s == 0) a.idx[c * (a.T + 1) + t] = e;
-  else a.idxq[3 * (c * a.T + t) + s - 1] = e;
-}
-
 __global__ __launch_bounds__(kThreads) void k_idx_emit(IdxArgs a) {
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= (int64_t)a.nclients * a.nchunks) return;
-  const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
-  const int64_t nbits = 8 * a.nbytes[c];
-  const int64_t cb = j * kIdxChunkBits, ce = cb + kIdxChunkBits;
-  if (cb >= nbits) return;  // (an empty code never ends: k_idx_check)
-  const int64_t s = j == 0 ? 0 : a.x2[g - 1];
-  if (s == kIdxFail) return;  // past the code's end
-  int64_t L = a.n2[g];        // the last nonzero before the chunk's first code
-  if (L >= a.P) return;       // (past the trailing run of a code with bytes after it)
-  const int gs = a.idxq ? 8 : 10;  // unit: quarter tile or tile
-  IdxReader r;
-  r.init(idx_words(a, c), nbits, s);
-  int64_t u = (L + ((int64_t)1 << gs)) >> gs;  // the first unit starting after L
-  int64_t bend = -1, total = -1;
-  bool bad = false;
-  for (;;) {
-    const int64_t p = r.pos;
-    if (p >= ce) break;  // the next chunk's lane continues
-    if (L == a.P - 1) {  // every element covered, no trailing run
-      bend = total = p;
-      break;
+  __shared__ __attribute__((aligned(16))) uint32_t lut[kLutSize];
+  idx_load_lut(lut);
+  const int64_t lanes = (int64_t)a.nclients * a.nchunks;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < lanes; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
+    const int64_t nbits = 8 * a.nbytes[c];
+    const int64_t cb = j * kIdxChunkBits, ce = cb + kIdxChunkBits;
+    if (cb >= nbits) continue;  // (an empty code never ends: k_idx_check)
+    const int64_t s = j == 0 ? 0 : a.x2[g - 1];
+    if (s == kIdxFail) continue;  // past the code's end
+    const int64_t L = a.n2[g];    // the last nonzero before the chunk's first code
+    if (L >= a.P) continue;       // (past the trailing run of a code with bytes after it)
+    IdxEnd end{-1, -1, false};
+    idx_parse<true>(a, c, lut, s, ce, L, &end);
+    if (end.bad) {
+      atomicOr(a.err, 1);
+    } else if (end.bend >= 0) {
+      if ((end.total + 7) / 8 != a.nbytes[c]) atomicOr(a.err, 1);  // bytes after the code, or a short final byte
+    } else if (ce >= nbits) {
+      atomicOr(a.err, 1);  // the code ends before its elements do
     }
-    const uint32_t d = idx_gamma(r);
-    if (!d || L + (int64_t)d > a.P) {
-      bad = true;
-      break;
-    }
-    if (L + (int64_t)d == a.P) {  // the trailing zero run
-      bend = p;
-      total = r.pos;
-      break;
-    }
-    r.refill();
-    if (r.nv < 1 || (r.skip(1), !idx_gamma(r))) {
-      bad = true;
-      break;
-    }
-    const int64_t nz = L + d;
-    const uint64_t e = ((uint64_t)p & kMask36) | ((uint64_t)(L + 1) << 36);
-    for (; (u << gs) <= nz; ++u) idx_put(a, c, u, e);
-    L = nz;
-  }
-  if (bad) {
-    atomicOr(a.err, 1);
-  } else if (bend >= 0) {
-    const uint64_t e = ((uint64_t)bend & kMask36) | ((uint64_t)(L + 1) << 36);
-    const int64_t nu = a.idxq ? 4 * (int64_t)a.T : (int64_t)a.T;
-    for (; u < nu; ++u) idx_put(a, c, u, e);
-    a.idx[c * (a.T + 1) + a.T] = e;
-    a.total_bits[c] = total;
-    a.ended[c] = 1;
-    if ((total + 7) / 8 != a.nbytes[c]) atomicOr(a.err, 1);  // bytes after the code, or a short final byte
-  } else if (ce >= nbits) {
-    atomicOr(a.err, 1);  // the code ends before its elements do
   }
 }
 
@@ -4317,6 +4423,73 @@ __global__ __launch_bounds__(256) void k_copy_f4(uint4* __restrict__ dst, const 
   for (; i < n; i += 256) dst[i] = src[i];
 }
 
+// Measurement kernel (not a reference interface; fc_quantize_floor): the encoder's
+// arithmetic floor -- read x, draw TF's Philox4x32-10 stream, the exact quantiser
+// (pow2 step: x * (1 / step); floor, ceil, Uint32ToFloat, compare, select; rintf
+// uniform) and the distortion FMA and nonzero count per 1024-element tile, with no
+// code construction, scan, look-back, emission or stores beyond two words per tile.
+// Persistent waves over tile-major tickets like the encoder's, keys per client
+// precomputed (k_floor_keys), all four chunk loads of a tile in flight at once.
+__global__ void k_floor_keys(const int64_t* seeds, int32_t C, uint4* keys) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const Key4 k = tf_seed_scramble(seeds[2 * c], seeds[2 * c + 1]);
+  keys[c] = make_uint4(k.k0, k.k1, k.c2, k.c3);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_quant_floor(const float* const* xs, int32_t C, int64_t P, int32_t T,
+                                                     float rcp, const uint4* keys, float* dist_part,
+                                                     int32_t* nnz_part) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t tickets = (int64_t)C * T;
+  for (int64_t tk = wave; tk < tickets; tk += nw) {
+    const int64_t t = tk / C;
+    const int32_t c = (int32_t)(tk - t * C);
+    const uint4 kk = keys[c];
+    const Key4 key{(uint32_t)__builtin_amdgcn_readfirstlane(kk.x), (uint32_t)__builtin_amdgcn_readfirstlane(kk.y),
+                   (uint32_t)__builtin_amdgcn_readfirstlane(kk.z), (uint32_t)__builtin_amdgcn_readfirstlane(kk.w)};
+    const float* x = xs[c];
+    float4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t e0 = t * kTE + 4 * (64 * j + lane);
+      v[j] = e0 + 3 < P ? *(const float4*)(x + e0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float dist = 0.0f;
+    int32_t nnz = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t g = (uint32_t)((t * kTE) >> 2) + 64 * j + lane;
+      uint4 rb = make_uint4(0, 0, 0, 0);
+      if (MODE != FC_UNIFORM) rb = philox_group_u(key, g);
+      const float xv[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+      const uint32_t rr[4] = {rb.x, rb.y, rb.z, rb.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float sc = xv[k] * rcp;
+        float r;
+        if (MODE == FC_UNIFORM) {
+          r = rintf(sc);
+        } else {
+          const float fl = floorf(sc);
+          r = (u01(rr[k]) <= sc - fl) ? ceilf(sc) : fl;
+        }
+        const float dd = sc - r;
+        dist = fmaf(dd, dd, dist);
+        nnz += (int32_t)__popcll(__ballot(r != 0.0f));
+      }
+    }
+    const float d = wave_sum_f(dist);
+    if (lane == 0) {
+      dist_part[(int64_t)c * T + t] = d;
+      nnz_part[(int64_t)c * T + t] = nnz;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host side.
 // ---------------------------------------------------------------------------
@@ -4383,7 +4556,8 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
                   void* workspace, int64_t workspace_bytes, void* stream, const int64_t* elem_off = nullptr,
                   int64_t max_cap = 0, uint64_t* idxq = nullptr) {
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
+  if (P <= 0 || P > FC_MAX_ROW_ELEMS)
+    return fail(-1, "P must be in [1, 2^26 - 1] for one encoder row; longer tensors: fc_quantize_encode_segmented");
   if (!xs || !stream_buf || !stream_off || !stream_cap || !idx || !total_bits || !overflow)
     return fail(-1, "null required pointer");
   if (!int_in && mode != FC_UNIFORM && !seeds) return fail(-1, "seeds required for stochastic/dithered");
@@ -4877,8 +5051,10 @@ struct SegLayout {
 bool seg_layout(int32_t C, int64_t P, int32_t K, int64_t max_cap, SegLayout& L) {
   if (C <= 0 || K < 1 || K > 63 || P <= 0 || max_cap <= 0) return false;
   L.seg_elems = P / K / 2048 * 2048;
-  if (L.seg_elems < 2048) return false;
+  if (L.seg_elems < 2048 || P > FC_MAX_ELEMS) return false;
   L.rem_elems = P - (int64_t)K * L.seg_elems;
+  // every segment is one encoder row (26-bit look-back positions)
+  if (L.seg_elems > FC_MAX_ROW_ELEMS || L.rem_elems > FC_MAX_ROW_ELEMS) return false;
   L.Tv = (int32_t)tiles_for(L.seg_elems);
   L.Tr = L.rem_elems > 0 ? (int32_t)tiles_for(L.rem_elems) : 0;
   L.nseg = K + (L.rem_elems > 0 ? 1 : 0);
@@ -4929,7 +5105,8 @@ int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float 
                      int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow, void* workspace,
                      int64_t workspace_bytes, void* stream, void* stitch_stream = nullptr) {
   SegLayout L;
-  if (!seg_layout(nclients, P, K, max_cap, L)) return fail(-1, "segmented encode: segments below 2048 elements");
+  if (!seg_layout(nclients, P, K, max_cap, L))
+    return fail(-1, "segmented encode: segments must hold 2048 .. 2^26 - 1 elements (P <= 2^28 - 1, K <= 63)");
   if (!xs || !stream_buf || !stream_off || !stream_cap || !idx || !total_bits || !overflow)
     return fail(-1, "null required pointer");
   if (!workspace || workspace_bytes < L.total || ((uintptr_t)workspace & 255))
@@ -5032,7 +5209,7 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
                   const uint64_t* idx, int32_t nclients, int64_t P, int32_t* err, void* stream,
                   int64_t tile_begin = 0, int64_t tile_end = -1, bool reset_err = true) {
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^28 - 1]");
   if (!stream_buf || !stream_off || !stream_cap || !idx || !err) return fail(-1, "null required pointer");
   a.stream_buf = stream_buf;
   a.stream_off = stream_off;
@@ -5097,7 +5274,7 @@ int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int6
                 int64_t P, int64_t max_bytes, uint64_t* idx, uint64_t* idxq, int64_t* total_bits, int32_t* err,
                 void* workspace, int64_t workspace_bytes, void* stream) {
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^28 - 1]");
   if (max_bytes < 0) return fail(-1, "max_bytes must be >= 0");
   if (!stream_buf || !stream_off || !nbytes || !idx || !total_bits || !err) return fail(-1, "null required pointer");
   if (!workspace || workspace_bytes < idx_workspace_bytes(nclients, max_bytes) || ((uintptr_t)workspace & 15))
@@ -5126,7 +5303,12 @@ int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int6
       hipMemsetAsync(a.ended, 0, 4 * (size_t)nclients, s) != hipSuccess)
     return fail(-10, "memset");
   const dim3 lgrid((unsigned)((lanes + kThreads - 1) / kThreads));
-  hipLaunchKernelGGL(k_idx_spec, lgrid, dim3(kThreads), 0, s, a);
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  // the table-driven parses: persistent workgroups (one table copy each)
+  const dim3 pgrid((unsigned)std::min<int64_t>((lanes + kThreads - 1) / kThreads, (int64_t)ncu * 8));
+  hipLaunchKernelGGL(k_idx_spec, pgrid, dim3(kThreads), 0, s, a);
   if (const int rc = check_launch("k_idx_spec")) return rc;
   hipLaunchKernelGGL(k_idx_sync, lgrid, dim3(kThreads), 0, s, a);
   if (const int rc = check_launch("k_idx_sync")) return rc;
@@ -5134,7 +5316,7 @@ int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int6
   if (const int rc = check_launch("k_idx_fix")) return rc;
   hipLaunchKernelGGL(k_idx_scan, dim3(nclients), dim3(64), 0, s, a);
   if (const int rc = check_launch("k_idx_scan")) return rc;
-  hipLaunchKernelGGL(k_idx_emit, lgrid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(k_idx_emit, pgrid, dim3(kThreads), 0, s, a);
   if (const int rc = check_launch("k_idx_emit")) return rc;
   hipLaunchKernelGGL(k_idx_check, dim3((unsigned)((nclients + 255) / 256)), dim3(256), 0, s, a);
   return check_launch("k_idx_check");
@@ -5354,7 +5536,7 @@ int fc_decode_accumulate_scaled_bounded(const uint8_t* stream_buf, const int64_t
                                         int32_t qmax, void* workspace, int64_t workspace_bytes, void* stream) {
   if (!out || !client_scale || !workspace) return fail(-1, "null required pointer");
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^28 - 1]");
   if ((uintptr_t)workspace & 15u) return fail(-1, "workspace must be 16-byte aligned");
   // |q| <= 127 declared: int8 rows (a quarter of the rows' memset / write / read traffic)
   const bool q8 = qmax > 0 && qmax <= 127;
@@ -5406,7 +5588,7 @@ int fc_vote_lengths(const float* const* xs, int32_t nclients, int64_t P, const f
                     const int64_t* seeds, int mode, int64_t* bits, double* dist, void* workspace,
                     int64_t workspace_bytes, void* stream) {
   if (nclients <= 0 || K <= 0) return fail(-1, "nclients and K must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^26 - 1]");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^28 - 1]");
   if (mode < 0 || mode > 2) return fail(-1, "mode must be 0 (uniform), 1 (stochastic) or 2 (dithered)");
   if (!xs || !steps || !bits || !dist || (mode != FC_UNIFORM && !seeds)) return fail(-1, "null required pointer");
   if (!workspace || workspace_bytes < fc_vote_workspace_bytes(nclients, P, K) || ((uintptr_t)workspace & 15))
@@ -5469,6 +5651,33 @@ int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, in
     L0 += k;
   }
   return 0;
+}
+
+int fc_quantize_floor(const float* const* xs, int32_t nclients, int64_t P, float step, const int64_t* seeds, int mode,
+                      float* dist_part, int32_t* nnz_part, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (nclients <= 0 || P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "bad nclients / P");
+  if (mode != FC_UNIFORM && mode != FC_STOCHASTIC) return fail(-1, "floor kernel: uniform or stochastic");
+  if (!xs || !seeds || !dist_part || !nnz_part || !workspace || workspace_bytes < 16LL * nclients)
+    return fail(-1, "null pointer or workspace below 16 bytes per client");
+  int e = 0;
+  const float m = std::frexp(step, &e);
+  if (!(step > 0.0f) || m != 0.5f) return fail(-1, "floor kernel: step must be a power of two");
+  hipStream_t s = (hipStream_t)stream;
+  uint4* keys = (uint4*)workspace;
+  hipLaunchKernelGGL(k_floor_keys, dim3((nclients + 255) / 256), dim3(256), 0, s, seeds, nclients, keys);
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int32_t T = (int32_t)tiles_for(P);
+  const int64_t waves = std::min<int64_t>((int64_t)nclients * T, (int64_t)ncu * 32);
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  if (mode == FC_UNIFORM)
+    hipLaunchKernelGGL(k_quant_floor<FC_UNIFORM>, grid, dim3(256), 0, s, xs, nclients, P, T, 1.0f / step, keys,
+                       dist_part, nnz_part);
+  else
+    hipLaunchKernelGGL(k_quant_floor<FC_STOCHASTIC>, grid, dim3(256), 0, s, xs, nclients, P, T, 1.0f / step, keys,
+                       dist_part, nnz_part);
+  return check_launch("k_quant_floor");
 }
 
 int fc_copy(void* dst, const void* src, int64_t nbytes, void* stream) {

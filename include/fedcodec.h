@@ -71,7 +71,12 @@ extern "C" {
 #define FC_NORM_L2_LINF 6 /* both wrapper norms in one pass: norms[c] = L2, norms[nclients + c] = LINF */
 
 #define FC_TILE_ELEMS 1024       /* encoder tile (one wavefront) = decoder index granularity */
-#define FC_MAX_ELEMS 67108863LL  /* P limit: 2^26 - 1 elements per client tensor */
+#define FC_MAX_ELEMS 268435455LL     /* P limit: 2^28 - 1 elements per client tensor (the decoder
+                                        index holds 1 + the last nonzero in 28 bits) */
+#define FC_MAX_ROW_ELEMS 67108863LL  /* one encoder row (26-bit positions in the look-back status):
+                                        fc_quantize_encode(_hinted / _quarters) and fc_rlgamma_encode
+                                        take P <= 2^26 - 1; fc_quantize_encode_segmented cuts longer
+                                        tensors into rows of at most this many elements */
 
 const char* fc_last_error(void);
 const char* fc_version(void);
@@ -226,7 +231,7 @@ int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off,
  * and total_bits, bit for bit what the encoder writes, after which
  * fc_decode_accumulate(_tiles / _quarters) decode the batch as usual.
  *   stream_off  device int64[nclients]: client c's code at stream_buf + stream_off[c]
- *               (4-byte aligned; readable up to the next 16-byte boundary past its end)
+ *               (16-byte aligned; readable up to the next 16-byte boundary past its end)
  *   nbytes      device int64[nclients]: each code's byte length (the tf.string's length)
  *   max_bytes   host: >= every nbytes[c] (sizes the work; fc_index_workspace_bytes)
  *   err         device int32[1]: cleared, then set nonzero on a malformed code (a code
@@ -352,6 +357,15 @@ int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, in
  * of 16, 16-byte aligned pointers; a grid-stride 16-byte-per-lane copy whose rate
  * bench.py reports as the achievable HBM streaming peak beside the codec kernels. */
 int fc_copy(void* dst, const void* src, int64_t nbytes, void* stream);
+
+/* Measurement utility (not a reference interface): the encoder's arithmetic floor
+ * -- read every x, draw TF's Philox4x32-10 stream, apply the exact quantiser
+ * (uniform or stochastic, power-of-two step) and sum the distortion and nonzeros
+ * per 1024-element tile into dist_part / nnz_part (layout of fc_quantize_encode's),
+ * with no run-length gamma coding.  workspace >= 16 * nclients bytes (16-byte
+ * aligned).  bench / DESIGN.md compare fc_quantize_encode's time with it. */
+int fc_quantize_floor(const float* const* xs, int32_t nclients, int64_t P, float step, const int64_t* seeds, int mode,
+                      float* dist_part, int32_t* nnz_part, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -195,3 +195,17 @@ def test_drive_create_and_builders():
     builder.build_drive_aggregator(rotation="dft")
   with pytest.raises(ValueError):
     builder.build_one_bit_sgd_aggregator(rotation="fft")
+
+
+def test_min_segments_bounds():
+  """Tensors longer than one encoder row (2^26 - 1) are always segmented, into rows
+  of at most that many elements; beyond the index's 2^28 - 1 elements: ValueError."""
+  from federated_amd import _lib, codec  # pylint: disable=g-import-not-at-top
+  assert codec.min_segments(_lib.MAX_ROW_ELEMS) == 1
+  for P in (_lib.MAX_ROW_ELEMS + 1, (1 << 26) + 5, 100_000_000, _lib.MAX_ELEMS):
+    k = codec.min_segments(P)
+    assert 2 <= k <= 63 and P // k // 2048 * 2048 <= _lib.MAX_ROW_ELEMS
+    assert P - k * (P // k // 2048 * 2048) <= _lib.MAX_ROW_ELEMS
+    assert codec.auto_segments(1024, P) >= k and codec.auto_segments(2, P) >= k
+  with pytest.raises(ValueError):
+    codec.min_segments(_lib.MAX_ELEMS + 1)
