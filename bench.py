@@ -68,7 +68,7 @@ from federated_amd import distributed  # noqa: E402
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 MODES = {"uniform": _lib.UNIFORM, "stochastic": _lib.STOCHASTIC, "dithered": _lib.DITHERED}
 EXTRA = ["headline_uniform", "trainer_round", "config2", "config3", "config4_share", "headline_c128", "onebit",
-         "copy"]
+         "onebit_c128", "copy"]
 
 
 def parse():
@@ -379,8 +379,9 @@ def w_trainer_round(rows, ptrs, P, steps, warmup, stream):
   }
 
 
-def w_onebit(rows, ptrs, P, steps, warmup, stream):
-  """Config 5's codec on one GPU: 1024 x 25 M one-bit SGD encode + client-order decode-sum."""
+def w_onebit(rows, ptrs, P, steps, warmup, stream, name="onebit"):
+  """Config 5's codec on one GPU: 1024 x 25 M one-bit SGD encode + client-order decode-sum
+  (name "onebit_c128": one GPU's 128-client share of config 5's 8-GPU run)."""
   C = len(rows)
   dev = rows[0].device
   nw = (P + 31) // 32
@@ -400,9 +401,9 @@ def w_onebit(rows, ptrs, P, steps, warmup, stream):
   t_step = ms["k_mask_encode"] + ms["k_onebit_decode_sum"]
   enc_bytes = C * 4.0 * P + C * 4.0 * nw
   return {
-      "workload": "onebit", "clients": C, "P": P, "codec": "one-bit SGD, threshold 0",
+      "workload": name, "clients": C, "P": P, "codec": "one-bit SGD, threshold 0",
       "ms_per_step": round(t_step, 3), "value_GiBps": round(C * P * 4.0 / (t_step * 1e-3) / 2**30, 2),
-      "roofline": roofline("k_mask_encode", enc_bytes, ms["k_mask_encode"], "onebit"),
+      "roofline": roofline("k_mask_encode", enc_bytes, ms["k_mask_encode"], name),
       "decode": {"kernel": "k_onebit_decode_sum", "launch_ms": round(ms["k_onebit_decode_sum"], 3),
                  "alg_GBps": round((C * 4.0 * nw + 4.0 * P) / (ms["k_onebit_decode_sum"] * 1e-3) / 1e9, 1)},
   }
@@ -434,6 +435,8 @@ def run_extra(name, args, dev, stream, head_rows, head_ptrs):
     return w_trainer_round(head_rows, head_ptrs, P, steps, warmup, stream)
   if name == "onebit":
     return w_onebit(head_rows, head_ptrs, P, steps, warmup, stream)
+  if name == "onebit_c128":  # config 5's per-GPU share at 8 GPUs: the first 128 client deltas
+    return w_onebit(head_rows[:128], head_ptrs[:128], P, max(steps, 10), warmup, stream, name="onebit_c128")
   if name == "copy":
     return w_copy(dev, stream)
   if name == "headline_c128":  # the first 128 of the headline's client deltas
@@ -555,7 +558,8 @@ def main():
   g.manual_seed(20251015 + rank)
   npool = args.pool if args.pool > 0 else Cg
   pool = []
-  need_head = not single or args.workload in ("headline_uniform", "trainer_round", "onebit", "headline_c128")
+  need_head = not single or args.workload in ("headline_uniform", "trainer_round", "onebit", "headline_c128",
+                                              "onebit_c128")
   for i in range(npool if need_head else 0):
     if npool == Cg:  # a delta per client, seeded by its global index: any --gpus N sums the same round
       g.manual_seed(20251015 + rank * Cg + i)

@@ -31,6 +31,7 @@ SIGNATURES = {
     "fc_quantize_encode": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P,
                                   _P, _P, _P, _P, _I64, _P]),
     "fc_rlgamma_encode": (_INT, [_P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "fc_rlgamma_encode_segmented": (_INT, [_P, _I32, _I64, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "fc_quantize_encode_hinted": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P,
                                          _P, _P, _P, _P, _I64, _I64, _P]),
     "fc_quantize_encode_quarters": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _INT, _P, _P, _P, _P, _P, _P,
@@ -65,6 +66,7 @@ SIGNATURES = {
     "fc_onebit_encode": (_INT, [_P, _I32, _I64, _F32, _P, _P, _P, _P]),
     "fc_drive_encode": (_INT, [_P, _I32, _I64, _INT, _P, _P, _P, _P]),
     "fc_hadamard": (_INT, [_P, _I32, _I64, _INT, _I64, _I64, _P]),
+    "fc_sign_flip": (_INT, [_P, _I32, _I64, _I64, _I64, _P]),
     "fc_onebit_decode_sum": (_INT, [_P, _P, _I32, _I64, _P, _P]),
     "fc_onebit_decode_sum_range": (_INT, [_P, _P, _I32, _I64, _I64, _I64, _P, _P]),
 }

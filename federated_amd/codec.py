@@ -482,7 +482,8 @@ class CapacityHint:
 
 
 def rlgamma_encode(qs, caps=None):
-  """tfc.run_length_gamma_encode over a batch of int32 tensors (device)."""
+  """tfc.run_length_gamma_encode over a batch of int32 tensors (device).  Tensors
+  longer than one encoder row are coded in segments and stitched (same bytes)."""
   _lib.require_gpu()
   rows = _rows(qs, torch.int32)
   P = rows[0].numel()
@@ -490,6 +491,14 @@ def rlgamma_encode(qs, caps=None):
   C = len(rows)
   ptrs = _ptr_array(rows, device)
   out = EncodedBatch(P, C, caps if caps is not None else [worst_case_capacity(P)] * C, device)
+  nseg = min_segments(P)
+  if nseg > 1:
+    max_cap = int(out.caps_host.max())
+    sws = _SEG_WS.get(C, P, nseg, max_cap, device)
+    _lib.call("fc_rlgamma_encode_segmented", _lib.ptr(ptrs), C, P, nseg, max_cap, _lib.ptr(out.stream),
+              _lib.ptr(out.stream_off), _lib.ptr(out.stream_cap), _lib.ptr(out.idx), _lib.ptr(out.total_bits),
+              _lib.ptr(out.overflow), _lib.ptr(sws), sws.numel(), _lib.stream_handle())
+    return out
   ws = _WS.get(C, P, device)
   _lib.call("fc_rlgamma_encode", _lib.ptr(ptrs), C, P, _lib.ptr(out.stream),
             _lib.ptr(out.stream_off), _lib.ptr(out.stream_cap), _lib.ptr(out.idx),
@@ -709,4 +718,36 @@ def hadamard_(rows, seed, inverse=False):
   ptrs = _ptr_array(rows, rows[0].device)
   _lib.call("fc_hadamard", _lib.ptr(ptrs), len(rows), n, int(bool(inverse)), int(seed[0]), int(seed[1]),
             _lib.stream_handle())
+  return rows
+
+
+def sign_flip_(rows, seed):
+  """In place x *= D (Rademacher signs of the Philox stream of ``seed``) for device rows."""
+  _lib.require_gpu()
+  ptrs = _ptr_array(rows, rows[0].device)
+  _lib.call("fc_sign_flip", _lib.ptr(ptrs), len(rows), rows[0].numel(), int(seed[0]), int(seed[1]),
+            _lib.stream_handle())
+  return rows
+
+
+def dft_(rows, seed, inverse=False):
+  """The DFT rotation of tff.aggregators.DiscreteFourierTransformFactory (builder.py:70-71)
+  on device rows of an even length n, in place: forward y = F(D x), with F the unitary
+  DFT of the n / 2 complex numbers x[:n/2] + i x[n/2:] returned as (real, imaginary)
+  halves; inverse x = D F^-1(y).  D: ``sign_flip_``; the FFT: torch.fft (rocFFT), a
+  library transform.  F is orthonormal, so the pair round-trips and preserves norms.
+  """
+  n = rows[0].numel()
+  if n % 2:
+    raise ValueError("the DFT rotation needs an even length (zero-pad first)")
+  h = n // 2
+  if not inverse:
+    sign_flip_(rows, seed)
+  for r in rows:
+    z = torch.complex(r[:h], r[h:])
+    z = torch.fft.fft(z, norm="ortho") if not inverse else torch.fft.ifft(z, norm="ortho")
+    r[:h] = z.real
+    r[h:] = z.imag
+  if inverse:
+    sign_flip_(rows, seed)
   return rows

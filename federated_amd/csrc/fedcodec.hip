@@ -4423,6 +4423,19 @@ __global__ __launch_bounds__(256) void k_copy_f4(uint4* __restrict__ dst, const 
   for (; i < n; i += 256) dst[i] = src[i];
 }
 
+// Rademacher sign flip (the DFT rotation's D, the same stream as k_fwht_pass's):
+// rows[c][i] *= sign of bit 31 of Philox output word i % 4 of counter i / 4.
+__global__ __launch_bounds__(256) void k_sign_flip(float* const* rows, int64_t n, Key4 key) {
+  float* x = rows[blockIdx.y];
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // 4-element group
+  if (4 * g >= n) return;
+  const uint4 r = philox_group(key, (uint32_t)g);
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (4 * g + k < n) x[4 * g + k] *= sign_of(w[k]);
+}
+
 // Measurement kernel (not a reference interface; fc_quantize_floor): the encoder's
 // arithmetic floor -- read x, draw TF's Philox4x32-10 stream, the exact quantiser
 // (pow2 step: x * (1 / step); floor, ceil, Uint32ToFloat, compare, select; rintf
@@ -5103,7 +5116,7 @@ int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float 
                      const float* prescale, const int64_t* seeds, int mode, int32_t K, int64_t max_cap,
                      uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
                      int64_t* total_bits, float* dist_part, int32_t* nnz_part, int32_t* overflow, void* workspace,
-                     int64_t workspace_bytes, void* stream, void* stitch_stream = nullptr) {
+                     int64_t workspace_bytes, void* stream, void* stitch_stream = nullptr, bool int_in = false) {
   SegLayout L;
   if (!seg_layout(nclients, P, K, max_cap, L))
     return fail(-1, "segmented encode: segments must hold 2048 .. 2^26 - 1 elements (P <= 2^28 - 1, K <= 63)");
@@ -5157,7 +5170,7 @@ int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float 
   if (const int rc = check_launch("k_seg_setup")) return rc;
   const int32_t nmain = nclients * K;
   int rc = encode_common((const void* const*)a.vptr, nmain, L.seg_elems, step, norms ? a.vnorms : nullptr,
-                         prescale ? a.vpre : nullptr, seeds ? a.vseeds : nullptr, mode, false, a.vstream,
+                         prescale ? a.vpre : nullptr, seeds ? a.vseeds : nullptr, mode, int_in, a.vstream,
                          a.vstream_off, a.vstream_cap, a.vidx_main, a.vbits, a.vdist_main, a.vnnz_main, a.vovf,
                          w + L.o_ws_main, L.o_ws_rem - L.o_ws_main, stream, a.voff,
                          std::min(L.vcap_main, max_cap * L.seg_elems / P + 8192));
@@ -5165,7 +5178,7 @@ int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float 
   if (L.rem_elems > 0) {
     rc = encode_common((const void* const*)(a.vptr + nmain), nclients, L.rem_elems, step,
                        norms ? a.vnorms + nmain : nullptr, prescale ? a.vpre + 2 * (int64_t)nmain : nullptr,
-                       seeds ? a.vseeds + 2 * (int64_t)nmain : nullptr, mode, false, a.vstream, a.vstream_off + nmain,
+                       seeds ? a.vseeds + 2 * (int64_t)nmain : nullptr, mode, int_in, a.vstream, a.vstream_off + nmain,
                        a.vstream_cap + nmain, a.vidx_rem, a.vbits + nmain, a.vdist_rem, a.vnnz_rem, a.vovf + nmain,
                        w + L.o_ws_rem, L.o_vptr - L.o_ws_rem, stream, a.voff + nmain,
                        max_cap * L.rem_elems / P + 8192);
@@ -5465,6 +5478,15 @@ int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P, uin
                        workspace, workspace_bytes, stream);
 }
 
+int fc_rlgamma_encode_segmented(const int32_t* const* qs, int32_t nclients, int64_t P, int32_t nseg, int64_t max_cap,
+                                uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
+                                int64_t* total_bits, int32_t* overflow, void* workspace, int64_t workspace_bytes,
+                                void* stream) {
+  return encode_segmented((const float* const*)qs, nclients, P, 1.0f, nullptr, nullptr, nullptr, FC_UNIFORM, nseg,
+                          max_cap, stream_buf, stream_off, stream_cap, idx, total_bits, nullptr, nullptr, overflow,
+                          workspace, workspace_bytes, stream, nullptr, true);
+}
+
 int64_t fc_index_workspace_bytes(int32_t nclients, int64_t max_bytes) {
   return nclients > 0 && max_bytes >= 0 ? idx_workspace_bytes(nclients, max_bytes) : -1;
 }
@@ -5628,6 +5650,15 @@ int fc_drive_encode(const float* const* xs, int32_t nclients, int64_t P, int min
   hipLaunchKernelGGL(k_mask_distortion<1>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, 0.0f,
                      (const float*)means, dist);
   return check_launch("k_mask_distortion<1>");
+}
+
+int fc_sign_flip(float* const* rows, int32_t nclients, int64_t n, int64_t seed0, int64_t seed1, void* stream) {
+  if (nclients <= 0 || nclients > 65535 || n <= 0 || n > (1LL << 34)) return fail(-1, "bad nclients / n");
+  if (!rows) return fail(-1, "null pointer");
+  const Key4 key = tf_seed_scramble(seed0, seed1);
+  const dim3 grid((unsigned)(((n + 3) / 4 + 255) / 256), (unsigned)nclients);
+  hipLaunchKernelGGL(k_sign_flip, grid, dim3(256), 0, (hipStream_t)stream, rows, n, key);
+  return check_launch("k_sign_flip");
 }
 
 int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, int64_t seed0, int64_t seed1,

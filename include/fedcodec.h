@@ -211,6 +211,16 @@ int fc_rlgamma_encode(const int32_t* const* qs, int32_t nclients, int64_t P,
                       int32_t* overflow, void* workspace, int64_t workspace_bytes,
                       void* stream);
 
+/* fc_rlgamma_encode of tensors longer than one encoder row (P up to
+ * FC_MAX_ELEMS): nseg segments per client (each at most FC_MAX_ROW_ELEMS and at
+ * least 2048 elements) encoded as rows and stitched into each client's one canonical
+ * code -- byte-identical to coding the tensor in one piece.  Workspace:
+ * fc_segmented_workspace_bytes(nclients, P, nseg, max_cap), 256-byte aligned. */
+int fc_rlgamma_encode_segmented(const int32_t* const* qs, int32_t nclients, int64_t P, int32_t nseg, int64_t max_cap,
+                                uint8_t* stream_buf, const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
+                                int64_t* total_bits, int32_t* overflow, void* workspace, int64_t workspace_bytes,
+                                void* stream);
+
 /* Decode nclients codes (layout as produced above) and sum them over clients.
  *   sum_in     nullable int32[P]: running sum to add to (multi-batch rounds)
  *   sum_out    nullable int32[P]: integer client sum (RCCL all-reduce input)
@@ -352,6 +362,12 @@ int fc_drive_encode(const float* const* xs, int32_t nclients, int64_t P, int min
  * the Rademacher signs of the Philox stream of (seed0, seed1). */
 int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, int64_t seed0,
                 int64_t seed1, void* stream);
+
+/* In place x *= D for nclients rows of n floats, D the Rademacher signs of the
+ * Philox stream of (seed0, seed1) (the stream fc_hadamard uses): the sign step of
+ * tff.aggregators.DiscreteFourierTransformFactory, which builder.py:70-71 wraps
+ * around a codec (the FFT itself is a library transform, rocFFT). */
+int fc_sign_flip(float* const* rows, int32_t nclients, int64_t n, int64_t seed0, int64_t seed1, void* stream);
 
 /* Measurement utility (not a reference interface): dst <- src, nbytes a multiple
  * of 16, 16-byte aligned pointers; a grid-stride 16-byte-per-lane copy whose rate

@@ -242,3 +242,24 @@ def hadamard_forward(x, seed):
 def hadamard_inverse(y, seed, P):
   n = y.size
   return (fwht(y) / np.sqrt(n) * rademacher(n, seed))[:P]
+
+
+def dft_forward(x, seed):
+  """DiscreteFourierTransformFactory's rotation as restated (builder.py:70-71; TFF's
+  own real/imaginary pairing unpinned): zero-pad to even n, signs D, then the unitary
+  DFT of the n/2 complex numbers x[:n/2] + i x[n/2:], (real, imaginary) halves."""
+  x = np.asarray(x, np.float32).reshape(-1)
+  n = x.size + (x.size % 2)
+  v = np.zeros(n, np.float64)
+  v[:x.size] = x
+  v *= rademacher(n, seed)
+  h = n // 2
+  z = np.fft.fft(v[:h] + 1j * v[h:], norm="ortho")
+  return np.concatenate([z.real, z.imag])
+
+
+def dft_inverse(y, seed, P):
+  y = np.asarray(y, np.float64).reshape(-1)
+  h = y.size // 2
+  z = np.fft.ifft(y[:h] + 1j * y[h:], norm="ortho")
+  return (np.concatenate([z.real, z.imag]) * rademacher(y.size, seed))[:P]

@@ -191,8 +191,8 @@ def test_drive_create_and_builders():
   assert isinstance(agg._inner, builder.HadamardTransformFactory)  # pylint: disable=protected-access
   from federated_amd.aggregators.comparison_methods import qsgd  # pylint: disable=g-import-not-at-top
   assert isinstance(builder.build_qsgd_aggregator(7.0)._inner, qsgd.QSGDFactory)  # pylint: disable=protected-access
-  with pytest.raises(NotImplementedError):
-    builder.build_drive_aggregator(rotation="dft")
+  assert isinstance(builder.build_drive_aggregator(rotation="dft")._inner,  # pylint: disable=protected-access
+                    builder.DiscreteFourierTransformFactory)
   with pytest.raises(ValueError):
     builder.build_one_bit_sgd_aggregator(rotation="fft")
 

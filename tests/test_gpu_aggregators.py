@@ -391,6 +391,48 @@ def test_hadamard_matches_oracle_and_round_trips(gpu, P):
   np.testing.assert_allclose(t.cpu().numpy()[:P], x, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("P", [1, 2, 3, 1000, 4097, 300_001])
+def test_dft_matches_oracle_and_round_trips(gpu, P):
+  """The DFT rotation (builder.py:70-71): signs from the same Philox stream as the
+  Hadamard rotation, unitary FFT of the n/2 complex numbers; against a float64
+  numpy restatement, norm-preserving, and inverted back to x."""
+  rng = np.random.default_rng(P + 1)
+  x = rng.standard_normal(P).astype(np.float32)
+  n = P + P % 2
+  t = torch.zeros(n, dtype=torch.float32, device=gpu)
+  t[:P] = torch.from_numpy(x).to(gpu)
+  codec.dft_([t], (7, 9))
+  y = t.cpu().numpy()
+  np.testing.assert_allclose(y, oagg.dft_forward(x, (7, 9)), rtol=1e-4, atol=1e-5 * max(1.0, np.log2(n)))
+  np.testing.assert_allclose(np.linalg.norm(y.astype(np.float64)), np.linalg.norm(x.astype(np.float64)), rtol=1e-5)
+  codec.dft_([t], (7, 9), inverse=True)
+  np.testing.assert_allclose(t.cpu().numpy()[:P], x, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("rotation", ["dft", "hadamard"])
+def test_quantize_encode_with_rotation_end_to_end(gpu, rotation):
+  """build_quantization_encode_aggregator(rotation=...) (builder.py:68-71): the round's
+  result is the weighted mean within the quantiser's error in the rotated basis,
+  and a linear inner aggregator makes the rotation invisible."""
+  rng = np.random.default_rng(9)
+  P, C = 3001, 4
+  xs = [(rng.standard_normal(P) * 0.1).astype(np.float32) for _ in range(C)]
+  agg = builder.build_quantization_encode_aggregator(step_size=0.001, rotation=rotation, zeroing=False,
+                                                     clipping=False, weighted=False)
+  process = agg.create((np.float32, (P,)))
+  out = process.next(process.initialize(), xs)
+  mean = np.mean(np.stack(xs), axis=0)
+  res = np.asarray(out.result)
+  assert res.shape == (P,)
+  assert np.max(np.abs(res - mean)) < 0.002  # |error| <= step / 2 per coordinate, rotated back
+  factory = builder.DiscreteFourierTransformFactory if rotation == "dft" else builder.HadamardTransformFactory
+  from federated_amd.aggregators import sum_factory  # pylint: disable=g-import-not-at-top
+  proc = factory(sum_factory.SumFactory()).create((np.float32, (P,)))
+  out = proc.next(proc.initialize(), xs)
+  np.testing.assert_allclose(np.asarray(out.result), np.sum(np.stack(xs).astype(np.float64), 0), rtol=1e-4,
+                             atol=1e-4)
+
+
 def test_drive_with_hadamard_rotation_end_to_end(gpu):
   rng = np.random.default_rng(8)
   P, C = 5000, 4

@@ -86,3 +86,23 @@ def test_unsegmented_row_limit_is_enforced(gpu):
               _lib.ptr(b.stream_off), _lib.ptr(b.stream_cap), _lib.ptr(b.idx), _lib.ptr(b.total_bits),
               _lib.ptr(b.dist_part), _lib.ptr(b.nnz_part), _lib.ptr(b.overflow), _lib.ptr(ws), ws.numel(),
               _lib.stream_handle())
+
+
+def test_elias_gamma_sum_beyond_one_encoder_row(gpu):
+  """EliasGammaEncodedSumFactory (elias_gamma_encode.py:57-116) on int32 tensors of
+  2^26 + 5 elements: the segmented rlgamma encode's bytes equal the oracle's TFC
+  code, and the round's sum is exact."""
+  from federated_amd.aggregators import elias_gamma_encode  # pylint: disable=g-import-not-at-top
+  P = (1 << 26) + 5
+  rng = np.random.default_rng(77)
+  qs = [np.clip(np.round(rng.standard_normal(P) * 3), -40, 40).astype(np.int32) for _ in range(2)]
+  qs[1][: P // 3] = 0  # a long zero run across segments
+  batch = codec.rlgamma_encode([torch.from_numpy(q).to(gpu) for q in qs])
+  for c in range(2):
+    assert batch.client_code(c) == ocodec.run_length_gamma_encode(qs[c])[0]
+  del batch
+  process = elias_gamma_encode.EliasGammaEncodedSumFactory().create((np.int32, (P,)))
+  out = process.next(process.initialize(), [torch.from_numpy(q).to(gpu) for q in qs])
+  got = np.asarray(out.result.cpu().numpy() if hasattr(out.result, "cpu") else out.result)
+  np.testing.assert_array_equal(got, qs[0] + qs[1])
+  torch.cuda.empty_cache()
