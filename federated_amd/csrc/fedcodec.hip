@@ -2647,7 +2647,12 @@ constexpr int kDecLongBits = FC_DEC_LONG_BITS;  // segment bits per element for 
 #define FC_DEC_ASYNC 1
 #endif
 constexpr bool kDecAsync = FC_DEC_ASYNC && kDecChunk == 1;
-struct SegReader {
+// ASYNC: batch-point loads the compiler does not track (k_decode, tuned); false:
+// plain loads the compiler waits for where their registers are used (the index
+// rebuild's reader: its control flow leaves the register allocator free to move an
+// untracked load's destination before the data lands).
+template <bool ASYNC>
+struct SegReaderT {
   const uint4* p;
   const uint4* end;
   uint4 cur[kDecChunk > 1 ? kDecChunk - 1 : 1];  // rest of the current chunk
@@ -2661,7 +2666,7 @@ struct SegReader {
   int32_t nwin, rb;
   int32_t vb;  // segment bits from the start of the next block taken (masks the last block)
   __device__ __forceinline__ void wait_nxt() {  // every outstanding load of the wave has landed
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(anx) :: "memory");
+    if (ASYNC && kDecAsync) asm volatile("s_waitcnt vmcnt(0)" : "+v"(anx) :: "memory");
   }
   __device__ __forceinline__ void load_async() {
     const uint4* q = p < end ? p : end - 1;  // clamped
@@ -2695,7 +2700,7 @@ struct SegReader {
       --cb;
       return;
     }
-    if (kDecAsync) {
+    if ((ASYNC && kDecAsync)) {
       if (!nv) {  // segment start, restart after a long code, or a lane far ahead
         load_async();
         wait_nxt();
@@ -2715,7 +2720,7 @@ struct SegReader {
     cb = kDecChunk - 1;
   }
   __device__ __forceinline__ void batch() {
-    if (kDecAsync) {
+    if ((ASYNC && kDecAsync)) {
       wait_nxt();  // the previous batch point's loads
       rdy = nv;
       if (!nv) {
@@ -2755,6 +2760,7 @@ struct SegReader {
     batch();
   }
 };
+using SegReader = SegReaderT<true>;
 
 // Decode table: the next 12 window bits -> up to two complete codes in one
 // 32-bit word, every field out with one AND or a constant shift pair:
@@ -3053,6 +3059,9 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     }
     if (stop) break;
   }
+  // the reader's last batch-point load may still be in flight into its register
+  // tuple: land it before the tuple dies (the registers are reused after the segment)
+  r.wait_nxt();
   // every decoded value must have landed inside this tile's accumulator
   bad |= (relb < lo_addr || relb >= hi_addr) ? 1u : 0u;
   if (bad || cons != total) atomicOr(err, 1);
@@ -3391,7 +3400,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
   // bits of the code from `start` on: a table / window code must end inside them (so
   // every path accepts exactly the codes the IdxReader does)
   const int32_t avail = (int32_t)min<int64_t>(nbits - start, (int64_t)lim + 8192);
-  SegReader r;
+  SegReaderT<false> r;
   auto restart = [&](int32_t cons) {
     r.init(base, cap, (uint64_t)(start + cons), (int32_t)min<int64_t>(nbits - start - cons, lim - cons + 8192));
     return cons + r.nwin;
@@ -3399,6 +3408,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
   int32_t cons = 0;
   int32_t fill = restart(0);
   uint32_t it = 0;
+  bool failed = false;
   while (cons < lim) {
     if ((++it & (kDecBatch - 1)) == 0) r.batch();
     const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
@@ -3457,7 +3467,8 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
         }
         if (!ok) {
           if (EMIT) end->bad = true;
-          return {kIdxFail, nsum};
+          failed = true;
+          break;
         }
         cons = (int32_t)(ir.pos - start);
         fill = restart(cons);
@@ -3479,6 +3490,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
       fill += 32;
     }
   }
+  if (failed) return {kIdxFail, nsum};
   if (EMIT) {
     L += acc4 >> 2;
     if (!end->bad && end->bend >= 0) {
