@@ -7,3 +7,4 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_bare_decode.py tests/test_g
 timeout -k 10 200 python3 tools/floor_bench.py > gpurun_out/floor.txt 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_idx3 -o idx -- python3 tools/index_bench.py > gpurun_out/index_bench3.txt 2>&1 || exit 3
 timeout -k 10 300 python3 tools/overlap_xbatch.py > gpurun_out/overlap_xbatch.txt 2>&1 || exit 4
+timeout -k 10 300 python3 tools/overlap_halves.py > gpurun_out/overlap_halves.txt 2>&1 || exit 5
