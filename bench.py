@@ -584,8 +584,15 @@ def main():
     import torch.distributed as dist  # pylint: disable=g-import-not-at-top
 
   bounds = distributed.slab_bounds(codec.num_tiles(P), args.slabs)  # shrinking: the last is smallest
+  # one GPU: the round in two client halves, the first half's decode beside the second
+  # half's encode (codec.encode_decode_pipelined; same int32 sum)
+  pipelined = world == 1 and codec.pipeline_wanted(Cg, P)
+  rnd = codec.PipelinedRound(P, list(batch.caps_host), dev) if pipelined else None
 
   def step():
+    if pipelined:
+      codec.encode_decode_pipelined(ptrs, P, args.step_size, seeds, mode, rnd, out=out, stream=stream)
+      return
     codec.quantize_encode(None, args.step_size, seeds, mode, ptrs=ptrs, P=P, out=batch,
                           stream=stream)
     if world == 1:
@@ -610,10 +617,10 @@ def main():
   for _ in range(args.warmup):
     step()
   torch.cuda.synchronize()
-  ovf = codec.check_overflow(batch)
+  ovf = rnd.overflowed() if pipelined else codec.check_overflow(batch)
   if len(ovf):
     raise SystemExit("stream capacity too small for %d clients; raise --cap-bytes-per-elem" % len(ovf))
-  if int(err.item()):
+  if int((rnd.err if pipelined else err).item()):
     raise SystemExit("decoder reported a malformed stream")
 
   # ---- timed region ----
@@ -685,7 +692,9 @@ def main():
                    "stream_capacity": "CapacityHint from an untimed probe round with other seeds" if not
                    args.cap_bytes_per_elem else "%g bytes per element" % args.cap_bytes_per_elem,
                    "parallelism": "client-sharded dp%d + RCCL int32 all-reduce"
-                   % world if world > 1 else "1 GPU"},
+                   % world if world > 1 else "1 GPU",
+                   "schedule": "two client halves: the first half's decode on a side stream beside the second "
+                               "half's encode" if pipelined else "encode, then decode"},
         "roofline": rl,
         "decode": {"kernel": "k_decode", "launch_ms": round(ms["k_decode"], 3),
                    "alg_GBps": round(dec_bytes / (ms["k_decode"] * 1e-3) / 1e9, 1)},

@@ -182,6 +182,82 @@ def decode_codes(codes, P, sum_in=None, want_sum=True, out=None, step=1.0, noise
   return s, o
 
 
+def pipeline_wanted(nclients, P):
+  """Whether a round runs as two client halves with the first half's decode overlapped
+  with the second half's encode (``encode_decode_pipelined``).  The super-tile
+  encoder keeps its per-client rate at 512 clients, so halving a large round costs
+  the encode little while the first decode hides under the second encode.
+  ``FEDCODEC_PIPELINE`` (0 / 1) overrides."""
+  import os  # pylint: disable=g-import-not-at-top
+  env = os.environ.get("FEDCODEC_PIPELINE")
+  if env:
+    return env != "0" and int(nclients) >= 2
+  return False
+
+
+class PipelinedRound:
+  """A round's clients as two EncodedBatches (halves [0, H) and [H, C)) and the
+  buffers of ``encode_decode_pipelined``; reused across rounds like an EncodedBatch."""
+
+  def __init__(self, P, caps, device):
+    C = len(caps)
+    self.P, self.nclients, self.H = int(P), C, C // 2
+    self.batches = (EncodedBatch(P, self.H, caps[:self.H], device),
+                    EncodedBatch(P, C - self.H, caps[self.H:], device))
+    self.partial = torch.empty(int(P), dtype=torch.int32, device=device)
+    self.err = torch.zeros(1, dtype=torch.int32, device=device)
+    self.device = device
+
+  def overflowed(self):
+    """Global indices of clients whose capacity was too small (host sync)."""
+    a, b = (check_overflow(x) for x in self.batches)
+    return np.concatenate([a, b + self.H])
+
+  def nbytes(self):
+    return np.concatenate([x.nbytes() for x in self.batches])
+
+
+def encode_decode_pipelined(ptrs, P, step, seeds, mode, rnd, out=None, sum_out=None, dq_step=None,
+                            noise_sum=None, norms=None, prescale=None, stream=None):
+  """One round: quantise + encode every client, decode + int32 sum + dequantise, in
+  two client halves with the first half's decode on a side stream beside the second
+  half's encode (kernel-boundary ordering only):
+      main: encode(A) -> encode(B) -> [wait] -> decode(B, sum_in = A's int32 sum) -> out
+      side:     [wait] decode(A) -> A's int32 sum
+  The same int32 sum and dequantised result as one encode + decode (integer sums).
+  ``rnd``: a PipelinedRound.  Returns rnd.err (zeroed and OR'ed here)."""
+  _lib.require_gpu()
+  main = stream if stream is not None else torch.cuda.current_stream()
+  side = _stitch_stream(rnd.device)
+  H, C = rnd.H, rnd.nclients
+  A, B = rnd.batches
+  seeds = torch.as_tensor(seeds, dtype=torch.int64).reshape(C, 2).to(rnd.device)
+  halves = ((0, H), (H, C))
+
+  def part(t, lo, hi, w=1):
+    return None if t is None else t.reshape(-1, w)[lo:hi].reshape(-1).contiguous()
+
+  with torch.cuda.stream(main):
+    rnd.err.zero_()
+    args = [(ptrs[lo:hi].contiguous(), seeds[lo:hi].contiguous(), part(norms, lo, hi), part(prescale, lo, hi, 2))
+            for lo, hi in halves]
+  quantize_encode(None, step, args[0][1], mode, ptrs=args[0][0], P=P, out=A, stream=main, norms=args[0][2],
+                  prescale=args[0][3])
+  ev = torch.cuda.Event()
+  ev.record(main)
+  side.wait_event(ev)
+  decode_accumulate(A, sum_out=rnd.partial, err=rnd.err, stream=side, tiles=(0, A.T))
+  done_a = torch.cuda.Event()
+  done_a.record(side)
+  quantize_encode(None, step, args[1][1], mode, ptrs=args[1][0], P=P, out=B, stream=main, norms=args[1][2],
+                  prescale=args[1][3])
+  main.wait_event(done_a)
+  dq = float(step if dq_step is None else dq_step)
+  decode_accumulate(B, sum_in=rnd.partial, sum_out=sum_out, want_sum=sum_out is not None, out=out, step=dq,
+                    noise_sum=noise_sum, err=rnd.err, stream=main, tiles=(0, B.T))
+  return rnd.err
+
+
 def split_stitch_wanted():
   """Whether a segmented batch stitches on a second stream while the round decodes
   the unstitched segments (fc_decode_accumulate_segmented).  Off by default
