@@ -152,11 +152,33 @@ def aggregate_round(local_rows, step, local_seeds, mode, group=None, prescale=No
   if multi is None:
     multi = is_multi(group)
   batch = None
+  out = None
+  if not multi and rows and codec.pipeline_wanted(len(rows), P):
+    # one process: the round in two client halves, the first half's decode beside the
+    # second half's encode; an overflowed capacity falls back to the checked path below
+    rnd = codec.PipelinedRound(P, list(caps) if caps is not None else [codec.default_capacity(P)] * len(rows),
+                               device)
+    ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=device)
+    noise = codec.noise_sum(local_seeds, P, device) if mode == _lib.DITHERED else None
+    out = torch.empty(P, dtype=torch.float32, device=device)
+    perr = codec.encode_decode_pipelined(
+        ptrs, P, step, local_seeds, mode, rnd, out=out, dq_step=dq, noise_sum=noise,
+        norms=norms, prescale=None if prescale is None else torch.as_tensor(prescale).reshape(-1, 2).to(device))
+    if not len(rnd.overflowed()):
+      if int(perr.item()):
+        raise RuntimeError("malformed run-length gamma code")
+      parts = [client_measurements(b, P) for b in rnd.batches]
+      distortion, sparsity, bits = (np.concatenate([p_[i] for p_ in parts]) for i in range(3))
+      meas = collections.OrderedDict(
+          avg_bitrate=np.float64(np.mean(bits) / np.float64(P)) if P else np.float64(0.0),
+          avg_distortion=F32(np.mean(distortion, dtype=np.float32)),
+          avg_sparsity=F32(np.mean(sparsity, dtype=np.float32)))
+      return RoundOutput(out, rnd, meas)
+    out = None
   if rows:
     batch = codec.quantize_encode_checked(rows, step, local_seeds, mode, norms=norms, caps=caps,
                                           prescale=prescale)
   err = torch.zeros(1, dtype=torch.int32, device=device)
-  out = None
   if not multi:
     out = (torch.empty if batch is not None else torch.zeros)(P, dtype=torch.float32, device=device)
     if batch is not None:

@@ -58,3 +58,29 @@ def test_pipelined_round_matches_oracle(gpu):
     acc += oq.stochastic_quantize(xs[c], F32(0.5), tuple(seeds[c]))
   want = oq.uniform_dequantize(acc.astype(np.int32), F32(0.5))
   np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("rounding", ["stochastic", "dithered"])
+def test_factory_round_pipelined_matches_oracle(gpu, monkeypatch, rounding):
+  """QuantizeEncodeFactory.next with the pipelined schedule on (FEDCODEC_PIPELINE=1):
+  the reference's result and measurements (quantize_encode.py:173-211), as the
+  in-order schedule gives them."""
+  from federated_amd.aggregators import quantize_encode  # pylint: disable=g-import-not-at-top
+  from oracle import aggregators as oagg  # pylint: disable=g-import-not-at-top
+  monkeypatch.setenv("FEDCODEC_PIPELINE", "1")
+  C, P = 7, 20_011
+  rng = np.random.default_rng(12)
+  xs = [(rng.standard_normal(P) * 0.8).astype(F32) for _ in range(C)]
+  seeds = np.array([[c + 1, 2 * c] for c in range(C)], np.int64)
+  process = quantize_encode.QuantizeEncodeFactory(0.5, rounding_type=rounding).create((np.float32, (P,)))
+  state = process.initialize()
+  for _ in range(2):  # the second round sizes its capacities from the first (CapacityHint)
+    out = process.next(state, xs, seeds=seeds)
+  want, meas, _ = oagg.quantize_encode_next(xs, 0.5, rounding, seeds=seeds)
+  if rounding == "dithered":
+    np.testing.assert_allclose(out.result, want, rtol=1e-6, atol=1e-6 * C)
+  else:
+    np.testing.assert_array_equal(np.asarray(out.result).view(np.uint32), want.view(np.uint32))
+  assert out.measurements["avg_bitrate"] == meas["avg_bitrate"]
+  np.testing.assert_allclose(out.measurements["avg_distortion"], meas["avg_distortion"], rtol=1e-5)
+  np.testing.assert_allclose(out.measurements["avg_sparsity"], meas["avg_sparsity"], rtol=1e-6)
