@@ -24,6 +24,8 @@ seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
 batch = codec.EncodedBatch(P, C, [2 * P + 1024] * C, dev)  # 16 bits per element
 codec.quantize_encode(None, STEP, seeds, _lib.STOCHASTIC, ptrs=ptrs, P=P, out=batch)
 out = torch.empty(P, dtype=torch.float32, device=dev)
+print("code bytes %d (%.3f bits per element)" % (int(batch.nbytes().sum()), 8.0 * batch.nbytes().sum() / (C * P)),
+      flush=True)
 for it in range(int(os.environ.get("ITERS", 3))):
   torch.cuda.synchronize()
   t0 = time.perf_counter()

@@ -9,9 +9,9 @@ passes) and the HBM bytes per launch with MI355X_MICROARCH.md's gfx950
 correction -- FETCH_SIZE x2 for wide (16-byte-per-lane) coalesced streaming
 reads (k_encode's LDS-DMA staging, the float4 row loads of k_client_norms and
 k_mask_encode -- each of their input bytes is read once, so the algorithmic
-bytes confirm the factor), FETCH_SIZE / 2.54 for the decoder's paced per-lane
-16-byte streams (calibrated on a known byte count: tools/microbench/fetch_calib.hip),
-plus WRITE_SIZE.  bench.py reads these
+bytes confirm the factor), FETCH_SIZE x1 for the decoder's per-lane 16-byte
+streams (the raw count: its excess over the code bytes is L2 re-fetch), plus
+WRITE_SIZE; the raw counts are recorded beside.  bench.py reads these
 files for the roofline's `traffic`.
 """
 import csv
@@ -25,11 +25,11 @@ from collections import defaultdict
 KERNELS = {  # name fragment -> (key, FETCH multiplier)
     "::k_encode<": ("k_encode", 2.0),
     "::k_encode2<": ("k_encode", 2.0),  # the super-tile variant (same LDS-DMA staging)
-    # the decoder's lanes stream their own segments in 16-byte loads paced by the decode:
-    # calibrated on a known byte count (tools/microbench/fetch_calib.hip, profiles/r03/
-    # fetch_calib.txt) FETCH_SIZE reads 2.54 x the bytes of that pattern when each byte
-    # is read exactly once (L2 misses tallied per 64-B request), so the bytes are FETCH / 2.54
-    "k_decode<": ("k_decode", 1.0 / 2.54),
+    # the decoder's lanes stream their own segments in 16-byte loads: the guide's
+    # correction is x1 (no wide coalesced streaming).  Round 3 divided by 2.54 (a
+    # calibration kernel of the same pattern); that hides real L2 re-fetch,
+    # so the raw x1 figure is the traffic and the calibrated one only a side note
+    "k_decode<": ("k_decode", 1.0),
     "k_client_norms": ("k_client_norms", 2.0),
     "k_mask_encode<": ("k_mask_encode", 2.0),
     "k_onebit_decode_sum": ("k_onebit_decode_sum", 1.0),
@@ -86,6 +86,7 @@ def main():
       write = sum(d["WRITE_SIZE"]) / max(1, len(d["WRITE_SIZE"]))
       m = mults[key]
       out[key] = {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write, "dispatches": len(d["FETCH_SIZE"]),
+                  "fetch_raw_bytes": fetch * 1024.0, "write_raw_bytes": write * 1024.0,
                   "fetch_multiplier": m, "hbm_bytes_corrected": (m * fetch + write) * 1024.0}
     out["workload"] = w
     out["command"] = "tools/profile_workloads.sh <out> %s (bench.py --workload %s)" % (w, w)
