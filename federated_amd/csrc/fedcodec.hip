@@ -1309,6 +1309,7 @@ __global__ void k_client_params(EncodeArgs a, ClientParam* cp, int need_key) {
   p.cap = a.stream_cap[c];
   p.gofs = a.elem_off ? a.elem_off[c] >> 2 : 0;
   cp[c] = p;
+  a.overflow[c] = 0;  // (instead of a memset launch: this kernel runs before every encoder kernel)
 }
 
 typedef const __attribute__((address_space(4))) ClientParam* ConstParamPtr;
@@ -4595,7 +4596,6 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   const int64_t T = tiles_for(P);
   const int64_t sb = enc_status_bytes(nclients, P);
   if (hipMemsetAsync(workspace, 0, enc_zeroed_bytes(nclients, P), s) != hipSuccess) return fail(-10, "memset status");
-  if (hipMemsetAsync(overflow, 0, sizeof(int32_t) * nclients, s) != hipSuccess) return fail(-10, "memset overflow");
   EncodeArgs a;
   a.elem_off = elem_off;
   a.idxq = idxq;
