@@ -3,8 +3,9 @@
 # FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md: one TCC counter group per
 # pass), per workload.  usage: bash tools/profile_workloads.sh <outdir> [workload ...]
 set -e
+set -o pipefail
 OUT=$1; shift
-WL=${@:-headline headline_uniform trainer_round config2 config3 config4_share headline_c128 onebit}
+WL=${@:-headline headline_uniform trainer_round config2 config3 config4_share headline_c128 onebit onebit_c128}
 export TMPDIR=/tmp
 mkdir -p $OUT
 for w in $WL; do
