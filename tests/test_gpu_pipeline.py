@@ -24,7 +24,7 @@ def test_pipelined_round_equals_plain_round(gpu, C, P, mode):
   ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=gpu)
   seeds = torch.tensor([[3 + c, 5 * c] for c in range(C)], dtype=torch.int64, device=gpu)
   pre = torch.from_numpy(np.stack([np.full(C, 0.9, F32), np.arange(1, C + 1, dtype=F32)], 1)).to(gpu)
-  caps = [codec.worst_case_capacity(P) // 4] * C
+  caps = [codec.worst_case_capacity(P)] * C  # (weights up to C: wide codes)
   noise = codec.noise_sum(seeds, P, gpu) if m == _lib.DITHERED else None
   plain = codec.quantize_encode(None, 0.25, seeds, m, ptrs=ptrs, P=P, caps=caps, prescale=pre)
   want_sum, want_out, err = codec.decode_accumulate(plain, out=torch.empty(P, device=gpu), step=0.25,
