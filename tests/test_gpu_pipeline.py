@@ -50,9 +50,10 @@ def test_pipelined_round_matches_oracle(gpu):
   rows = [torch.from_numpy(x).to(gpu) for x in xs]
   ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=gpu)
   seeds = np.array([[70 + c, c] for c in range(C)], np.int64)
-  rnd = codec.PipelinedRound(P, [codec.default_capacity(P)] * C, gpu)
+  rnd = codec.PipelinedRound(P, [codec.worst_case_capacity(P)] * C, gpu)
   out = torch.empty(P, dtype=torch.float32, device=gpu)
-  codec.encode_decode_pipelined(ptrs, P, 0.5, torch.from_numpy(seeds), _lib.STOCHASTIC, rnd, out=out)
+  e = codec.encode_decode_pipelined(ptrs, P, 0.5, torch.from_numpy(seeds), _lib.STOCHASTIC, rnd, out=out)
+  assert not len(rnd.overflowed()) and int(e.item()) == 0
   acc = np.zeros(P, np.int64)
   for c in range(C):
     acc += oq.stochastic_quantize(xs[c], F32(0.5), tuple(seeds[c]))
