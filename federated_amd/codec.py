@@ -278,37 +278,53 @@ def _stitch_stream(device):
   return _STITCH_STREAMS[key]
 
 
+def _stream_key(device, stream):
+  s = stream if stream is not None else torch.cuda.current_stream(device)
+  return (torch.device(device).index or 0, s.cuda_stream)
+
+
 class Workspace:
-  """Grow-only device workspace for the encoder's look-back status array."""
+  """Grow-only device workspace for the encoder's look-back status array, one per
+  stream: encodes on different streams may run at once and must not share the
+  status words and ticket counters (an encode on a stream is ordered only after
+  earlier work of that stream)."""
 
   def __init__(self):
-    self.buf = None
+    self.bufs = {}
 
-  def get(self, nclients, P, device):
+  def get(self, nclients, P, device, stream=None):
     need = int(_lib.load().fc_encode_workspace_bytes(int(nclients), int(P)))
-    if self.buf is None or self.buf.numel() < need or self.buf.device != device:
-      self.buf = torch.empty(_round_up(need, 256), dtype=torch.uint8, device=device)
-    return self.buf
+    key = _stream_key(device, stream)
+    buf = self.bufs.get(key)
+    if buf is None or buf.numel() < need:
+      self.bufs[key] = None
+      buf = torch.empty(_round_up(need, 256), dtype=torch.uint8, device=device)
+      self.bufs[key] = buf
+    return buf
 
 
 _WS = Workspace()
 
 
 class SegWorkspace:
-  """Grow-only device workspace of the segmented encoder (256-byte aligned)."""
+  """Grow-only device workspace of the segmented encoder (256-byte aligned), one per
+  stream (as Workspace)."""
 
   def __init__(self):
-    self.buf = None
+    self.bufs = {}
 
-  def get(self, nclients, P, nseg, max_cap, device):
+  def get(self, nclients, P, nseg, max_cap, device, stream=None):
     need = int(_lib.load().fc_segmented_workspace_bytes(int(nclients), int(P), int(nseg), int(max_cap)))
     if need < 0:
       return None
-    if self.buf is None or self.buf.numel() < need + 256 or self.buf.device != device:
-      self.buf = None
-      self.buf = torch.empty(_round_up(need + 256, 256), dtype=torch.uint8, device=device)
-    off = (-self.buf.data_ptr()) % 256
-    return self.buf[off:off + need]
+    key = _stream_key(device, stream)
+    buf = self.bufs.get(key)
+    if buf is None or buf.numel() < need + 256:
+      self.bufs[key] = None
+      buf = torch.empty(_round_up(need + 256, 256), dtype=torch.uint8, device=device)
+      self.bufs[key] = buf
+    off = (-buf.data_ptr()) % 256
+    return buf[off:off + need]
 
 
 _SEG_WS = SegWorkspace()
@@ -417,7 +433,7 @@ def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, p
   if nseg > 1:
     max_cap = int(out.caps_host.max())
     split = split_stitch_wanted()
-    sws = out.seg_workspace(nseg, max_cap) if split else _SEG_WS.get(C, P, nseg, max_cap, device)
+    sws = out.seg_workspace(nseg, max_cap) if split else _SEG_WS.get(C, P, nseg, max_cap, device, stream)
     if sws is None and nseg > 1 and P > _lib.MAX_ROW_ELEMS:
       raise ValueError("cannot segment %d elements into %d segments" % (P, nseg))
     if sws is not None:
@@ -435,7 +451,7 @@ def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, p
         ev.record(side)
         out._pending = ev
       return out
-  ws = _WS.get(C, P, device)
+  ws = _WS.get(C, P, device, stream)
   if quarter_index_wanted(C, nseg) if quarters is None else quarters:
     _lib.call("fc_quantize_encode_quarters", _lib.ptr(ptrs), C, P, float(step), _lib.ptr(norms),
               _lib.ptr(prescale), _lib.ptr(seeds), int(mode), _lib.ptr(out.stream), _lib.ptr(out.stream_off),

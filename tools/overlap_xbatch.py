@@ -30,6 +30,7 @@ caps = [int(P * 0.56)] * C
 A = codec.EncodedBatch(P, C, caps, dev)
 B = codec.EncodedBatch(P, C, caps, dev)
 codec.quantize_encode(None, 0.5, sa, _lib.STOCHASTIC, ptrs=ptrs, P=P, out=A)
+torch.cuda.synchronize()  # (A's encode done before any encode on another stream starts)
 out = torch.empty(P, dtype=torch.float32, device=dev)
 s1 = torch.cuda.Stream()
 s2 = torch.cuda.Stream()
