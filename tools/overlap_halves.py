@@ -54,12 +54,19 @@ def halves():
   codec.decode_accumulate(B, sum_in=sumA, sum_out=sum2, out=out, step=0.5, stream=s1)
 
 
+A_GRID = None  # the side decode's workgroups only (FEDCODEC_DEC_GRID around that launch)
+
+
 def overlapped():
   codec.quantize_encode(None, 0.5, sa, _lib.STOCHASTIC, ptrs=pa, P=P, out=A, stream=s1)
   e1 = torch.cuda.Event()
   e1.record(s1)
   s2.wait_event(e1)
+  if A_GRID:
+    os.environ["FEDCODEC_DEC_GRID"] = str(A_GRID)
   codec.decode_accumulate(A, sum_out=sumA, stream=s2)
+  if A_GRID:
+    os.environ.pop("FEDCODEC_DEC_GRID", None)
   e2 = torch.cuda.Event()
   e2.record(s2)
   codec.quantize_encode(None, 0.5, sb, _lib.STOCHASTIC, ptrs=pb, P=P, out=B, stream=s1)
@@ -87,13 +94,17 @@ def setenv(k, v):
 t1 = timeit(one_stream)
 th = timeit(halves)
 print("one stream %.2f ms   halves in order %.2f ms" % (t1, th), flush=True)
-for dg, eg in [(None, None), (256, None), (512, None), (768, None), (256, 3072), (512, 3072)]:
+for dg, eg in [(None, None), (768, None)]:
   setenv("FEDCODEC_DEC_GRID", dg)
   setenv("FEDCODEC_ENC_GRID", eg)
   to = timeit(overlapped)
   print("overlapped: dec grid %-5s enc grid %-5s %.2f ms" % (dg, eg, to), flush=True)
 setenv("FEDCODEC_DEC_GRID", None)
 setenv("FEDCODEC_ENC_GRID", None)
+for ag in (256, 384, 512, 768):
+  A_GRID = ag
+  print("overlapped: side decode grid %d only: %.2f ms" % (ag, timeit(overlapped)), flush=True)
+A_GRID = None
 one_stream()
 overlapped()
 torch.cuda.synchronize()
