@@ -1,0 +1,20 @@
+"""CPU guard (no GPU): the decoder's untracked inline-asm loads keep their destination
+registers untouched until their asm wait (tools/audit_async_loads.py; the fault class
+that took down a GPU run in round 4)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import audit_async_loads  # noqa: E402  pylint: disable=g-import-not-at-top
+
+
+def test_no_untracked_load_register_is_touched_before_its_wait(tmp_path):
+  path = str(tmp_path / "fedcodec.s")
+  audit_async_loads.assemble(path)
+  rep = audit_async_loads.audit(path)
+  assert any("k_decode" in k for k in rep), "the decoder's batch-point loads were not found"
+  assert not any("k_idx_" in k for k in rep), "the index rebuild must use the tracked reader"
+  bad = {k: v for k, v in rep.items() if v[1]}
+  assert not bad, bad
