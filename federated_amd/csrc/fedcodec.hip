@@ -54,6 +54,29 @@ constexpr uint32_t kNoPos = 0x1FFF; // "no nonzero" in a 13-bit tile-relative fi
 // (MI355X_MICROARCH.md "dequeue"), so tickets come from kTicketShards counters,
 // one 64-B line each; stream k hands out tickets k, k + K, k + 2K, ... in order.
 constexpr int kTicketShards = 32;
+#ifndef FC_XCD_SHARD
+#define FC_XCD_SHARD 0  // measured neutral (profiles/r04/diag_xcd_streams.txt): off
+#endif
+// Ticket stream of wave w of workgroup b.  XCD groups (workgroups are dealt
+// round-robin over the 8 XCDs, so b % 8 names the group; speed only): stream
+// k is drawn by one group's waves only (k % 8 == b % 8), so with the client
+// count a multiple of 8 -- client = ticket mod C -- every tile of a client is
+// coded on one XCD and the partial lines its tickets share (the code words
+// at ticket boundaries, the per-tile index / distortion / nonzero slots,
+// statuses) merge in that XCD's L2 instead of being written back once per XCD.
+__device__ __forceinline__ uint32_t ticket_shard(uint32_t b, uint32_t w, uint32_t wpg, uint32_t nshards,
+                                                 uint32_t xcd) {
+  if (xcd) return (b & 7u) + 8u * (((b >> 3) * wpg + w) % (nshards >> 3));
+  return (b * wpg + w) % nshards;
+}
+#ifndef FC_STORE_ALIGN
+#define FC_STORE_ALIGN 1
+#endif
+// Code-word stores line-aligned: lane l of a store instruction writes the word
+// at lane offset l from the 128-B line holding the ticket's first word, so each
+// instruction covers two whole lines instead of straddling three (the encoder's
+// WRITE_SIZE was 1.15x the code bytes with unaligned 256-B store instructions).
+constexpr bool kStoreAlign = FC_STORE_ALIGN;
 #ifndef FC_LOOKBACK_WIN
 #define FC_LOOKBACK_WIN 0  // 0: chosen per launch from the tiles in flight per client
 #endif
@@ -245,6 +268,14 @@ __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Both granules of a look-back status in one 16-byte store (readers accept a
+// status only once both carry the same flag, so the granule order is free).
+__device__ __forceinline__ void st_agent2(uint64_t* p, uint64_t g0, uint64_t g1) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = {(uint32_t)g0, (uint32_t)(g0 >> 32), (uint32_t)g1, (uint32_t)(g1 >> 32)};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
 // ---------------------------------------------------------------------------
@@ -271,6 +302,7 @@ struct EncodeArgs {
   uint64_t* status;   // [nclients * T][2]
   uint32_t* counter;  // kTicketShards ticket counters, 64 B apart (zeroed per launch)
   uint32_t nshards;   // ticket streams in use: min(kTicketShards, grid)
+  uint32_t xcd_shard; // streams by XCD group (host-checked: every stream has waves)
   uint32_t* spin_err;
   const void* cparams;   // ClientParam[nclients] (workspace)
   uint32_t* slow_count;  // clients handed to the exact kernel
@@ -1607,7 +1639,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
   for (int i = lane; i < 2 * (kWinWords + 3); i += kEncThreads) (&wins[0][0])[i] = 0;
-  const uint32_t shard = blockIdx.x % a.nshards;
+  const uint32_t shard = ticket_shard(blockIdx.x, 0, 1, a.nshards, a.xcd_shard);
   uint32_t* my_counter = a.counter + kShardStride * shard;
   // Tickets run two ahead: the tile after the current one is known when the
   // current one starts, so its values are staged into LDS (LDS-DMA) while the
@@ -1828,13 +1860,11 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
             agg.body = body;
             agg.tail = agg_tail;
             const Seg incl = seg_combine(root, agg);
-            st_agent(st + 1, kFlagPre | incl.tail);
-            st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+            st_agent2(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36), kFlagPre | incl.tail);
           } else {
             const uint64_t fr = tile_last >= 0 ? (uint64_t)tile_first : kNoPos;
             const uint64_t lr = tile_last >= 0 ? (uint64_t)tile_last : kNoPos;
-            st_agent(st + 1, kFlagAgg | agg_tail);
-            st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
+            st_agent2(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body, kFlagAgg | agg_tail);
           }
         }
         nv = true;
@@ -1910,8 +1940,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         }
         if (lane == 0) {
           if (pt > 0) {
-            st_agent(st + 1, kFlagPre | incl.tail);
-            st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+            st_agent2(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36), kFlagPre | incl.tail);
           }
           const int64_t ib = (int64_t)pc * (a.T + 1);
           a.idx[ib + pt] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
@@ -1933,11 +1962,14 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         const uint64_t w0 = excl.body >> 5;
         if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&enc_args_fresh().overflow[pc], 1u);
         const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
+        const uint32_t lead = kStoreAlign ? (uint32_t)(((uintptr_t)(out32 + w0) >> 2) & 31u) : 0u;  // lanes before the line
         if (!(FC_ABL & 1024))
-        for (uint32_t k = lane; k < nwords_owned; k += kEncThreads) {
-          const uint32_t wv32 = win_bits32(win, s0 + 32 * k);
+        for (uint32_t k = lane; k < nwords_owned + lead; k += kEncThreads) {
+          if (k < lead) continue;
+          const uint32_t kk = k - lead;
+          const uint32_t wv32 = win_bits32(win, s0 + 32 * kk);
           if (FC_ABL & 2) asm volatile("" :: "v"(wv32));
-          else if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
+          else if ((int64_t)(w0 + kk + 1) * 4 <= cap) out32[w0 + kk] = bswap32(wv32);
         }
         const uint32_t nt = min((uint32_t)kWinWords, (kPre + pbody + trail_len + 31) / 32 + 1);
         if (!(FC_ABL & 1024))
@@ -2037,7 +2069,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
   const uint32_t total = (uint32_t)a.nclients * (uint32_t)a.T2;
   const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
   const int64_t P = a.P;
-  const uint32_t shard = (blockIdx.x * kEnc2Waves + (uint32_t)wave) % a.nshards;
+  const uint32_t shard = ticket_shard(blockIdx.x, (uint32_t)wave, kEnc2Waves, a.nshards, a.xcd_shard);
   uint32_t* my_counter = a.counter + kShardStride * shard;
   // tickets run one ahead: the next super-tile's first tile is staged while the
   // current one's second tile computes
@@ -2270,15 +2302,10 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     if (fast) {
       const float d = DIV == 1 ? dsum * (cq.step * cq.step) : dsum;  // DIV 1: sums of (sc - r)^2
       const int32_t n = INT_IN ? wave_sum_i(nnz) : nnz;
-      if (lane == 0) {  // one partial per super-tile (its second tile's slot: 0)
-        if (a.dist_part) {
-          a.dist_part[(int64_t)c * a.T + t0] = d;
-          for (int h = 1; h < nt; ++h) a.dist_part[(int64_t)c * a.T + t0 + h] = 0.0f;
-        }
-        if (a.nnz_part) {
-          a.nnz_part[(int64_t)c * a.T + t0] = n;
-          for (int h = 1; h < nt; ++h) a.nnz_part[(int64_t)c * a.T + t0 + h] = 0;
-        }
+      // one partial per super-tile (its later tiles' slots: 0), one store instruction each
+      if (lane < nt) {
+        if (a.dist_part) a.dist_part[(int64_t)c * a.T + t0 + lane] = lane == 0 ? d : 0.0f;
+        if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t0 + lane] = lane == 0 ? n : 0;
       }
     }
     const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;
@@ -2296,15 +2323,13 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         excl.first = excl.last = -1;
         if (lane == 0) {
           const Seg incl = seg_combine(excl, agg);
-          st_agent(st + 1, kFlagPre | incl.tail);
-          st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+          st_agent2(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36), kFlagPre | incl.tail);
         }
       } else {
         if (lane == 0) {
           const uint64_t fr = slast >= 0 ? (uint64_t)sfirst : kNoPos;
           const uint64_t lr = slast >= 0 ? (uint64_t)slast : kNoPos;
-          st_agent(st + 1, kFlagAgg | agg_tail);
-          st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
+          st_agent2(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body, kFlagAgg | agg_tail);
         }
         STAMP(5);
         excl = lookback_vec<STE>(a.status + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2);
@@ -2338,24 +2363,21 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           trail_len = 2u * (63u - (uint32_t)__clzll(trail)) + 1u;
         }
       }
-      if (lane == 0) {
-        if (t2 > 0) {
-          st_agent(st + 1, kFlagPre | incl.tail);
-          st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
-        }
-        const int64_t ib = (int64_t)c * (a.T + 1);
-        a.idx[ib + t0] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
+      {  // decoder index entries of the super-tile's tiles (+ the row's end entry), lane h: tile t0 + h
+        uint64_t ie = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
 #pragma unroll
         for (int h = 1; h < NT; ++h) {  // later tiles: after the earlier tiles' codes (and the run code before them)
-          if (h >= nt) break;
           const uint64_t off = excl.body + (lastb[h] >= 0 ? (uint64_t)R0 + bodyb[h] : 0u);
           const int32_t lb = lastb[h] >= 0 ? (int32_t)(sbase + lastb[h]) : excl.last;
-          a.idx[ib + t0 + h] = (off & kMask36) | ((uint64_t)(lb + 1) << 36);
+          ie = lane == h ? (off & kMask36) | ((uint64_t)(lb + 1) << 36) : ie;
         }
-        if (last_st) {
-          a.idx[ib + a.T] = (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36);
-          enc_args_fresh().total_bits[c] = (int64_t)incl.body + trail_len;
-        }
+        ie = lane == nt ? (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36) : ie;  // (last_st only)
+        if (lane < nt + (last_st ? 1 : 0)) a.idx[(int64_t)c * (a.T + 1) + t0 + lane] = ie;
+      }
+      if (lane == 0) {
+        if (t2 > 0)
+          st_agent2(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36), kFlagPre | incl.tail);
+        if (last_st) enc_args_fresh().total_bits[c] = (int64_t)incl.body + trail_len;
         // leading pieces just before the body, trailing code after it
         emit64<kWin2Words>(win, tb, r0, kPre - bstart);
         emit64<kWin2Words>(win, dfirst, R0, kPre - R0);
@@ -2369,10 +2391,13 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       const uint64_t w0 = excl.body >> 5;
       if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&enc_args_fresh().overflow[c], 1u);
       const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
-      for (uint32_t k = lane; k < nwords_owned; k += kEncThreads) {
-        const uint32_t wv32 = win_bits32(win, s0 + 32 * k);
+      const uint32_t lead = kStoreAlign ? (uint32_t)(((uintptr_t)(out32 + w0) >> 2) & 31u) : 0u;  // lanes before the line
+      for (uint32_t k = lane; k < nwords_owned + lead; k += kEncThreads) {
+        if (k < lead) continue;
+        const uint32_t kk = k - lead;
+        const uint32_t wv32 = win_bits32(win, s0 + 32 * kk);
         if (FC_ABL & 2) asm volatile("" :: "v"(wv32));  // diagnostics: no stream stores
-        else if ((int64_t)(w0 + k + 1) * 4 <= cap) out32[w0 + k] = bswap32(wv32);
+        else if ((int64_t)(w0 + kk + 1) * 4 <= cap) out32[w0 + kk] = bswap32(wv32);
       }
       const uint32_t nt = min(kWin2Words, (kPre + body + trail_len + 31) / 32 + 1);
       for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
@@ -2463,8 +2488,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
       if (lane == 0) {
         const uint64_t fr = agg.has_nz ? (uint64_t)tile_first : kNoPos;
         const uint64_t lr = agg.has_nz ? (uint64_t)tile_last : kNoPos;
-        st_agent(st + 1, kFlagAgg | agg.tail);
-        st_agent(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body);
+        st_agent2(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body, kFlagAgg | agg.tail);
       }
       bool slow = false;
       excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, slow);
@@ -2487,8 +2511,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
       }
     }
     if (lane == 0) {
-      st_agent(st + 1, kFlagPre | incl.tail);
-      st_agent(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36));
+      st_agent2(st, kFlagPre | ((uint64_t)(incl.last + 1) << 36) | (incl.body & kMask36), kFlagPre | incl.tail);
       const int64_t ib = (int64_t)c * (a.T + 1);
       a.idx[ib + t] = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
       if (last_tile) {
@@ -4718,6 +4741,12 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   if (const char* g = getenv("FEDCODEC_ENC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
   const int grid = (int)std::min<int64_t>(tickets, max_grid);  // waves
   a.nshards = (uint32_t)std::min(kTicketShards, grid);
+  {  // XCD-group streams when each group's waves cover its nshards / 8 streams
+    const int64_t nblocks = (grid + wpg - 1) / wpg;
+    bool want = FC_XCD_SHARD;
+    if (const char* e = getenv("FEDCODEC_XCD_SHARD")) want = atoi(e) != 0;  // test knob
+    a.xcd_shard = want && a.nshards % 8 == 0 && (nblocks / 8) * wpg >= (int64_t)a.nshards / 8;
+  }
   {  // look-back prefetch window: 64 statuses when few tiles of a client are in flight,
      // 16 when many are (measured at 25 M: C = 128 -13 %, C = 1024 +2 % with 16)
     int win = kLookbackWin;
