@@ -71,39 +71,45 @@ def main():
     ks = glob.glob(os.path.join(base, "kt", "**", "*kernel_stats.csv"), recursive=True)
     if ks:
       shutil.copy(ks[0], os.path.join(dst, "kernel_stats_%s.csv" % w))
-    # per kernel key, per template instance: the untimed capacity-probe round launches
-    # another instance (two-tile tickets at an unknown capacity) whose counts must not
-    # be averaged into the timed instance's (round 3's records mixed them)
+    # per kernel key, per template instance.  Each instance's first dispatch in a pass is
+    # dropped: the untimed capacity-probe round (bench.py) launches first, sometimes as
+    # another instance (two-tile tickets at an unknown capacity) -- round 3's records
+    # averaged it into the timed launches.  A step may launch several instances of one
+    # kernel (segmented rounds: the super-tile main segments and the one-tile
+    # remainders); the instances launched about as often as the most frequent are the timed ones and their
+    # per-dispatch bytes add up to the step's.
     per = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
     mults = {}
     for f in glob.glob(os.path.join(base, "**", "*counter_collection.csv"), recursive=True):
       with open(f) as fh:
-        rows = [(int(r["Dispatch_Id"]), r) for r in csv.DictReader(fh)]
-      first = {}  # each pass's first dispatch per kernel key: the capacity probe (untimed), dropped
-      for did, row in rows:
+        rows = sorted(((int(r["Dispatch_Id"]), r) for r in csv.DictReader(fh)), key=lambda x: x[0])
+      seen = set()
+      for _, row in rows:
         k = kernel_key(row["Kernel_Name"])
-        if k:
-          first[k[0]] = min(first.get(k[0], did), did)
-      for did, row in rows:
-        k = kernel_key(row["Kernel_Name"])
-        if k and did != first[k[0]]:
-          per[k[0]][row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
-          mults[k[0]] = k[1]
+        if not k:
+          continue
+        if row["Kernel_Name"] not in seen:
+          seen.add(row["Kernel_Name"])
+          continue
+        per[k[0]][row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+        mults[k[0]] = k[1]
     out = {}
+    mean = lambda v: sum(v) / max(1, len(v))
     for key, inst in per.items():
-      # the timed instance: the one with the most dispatches
-      name = max(inst, key=lambda n: len(inst[n]["FETCH_SIZE"]) + len(inst[n]["WRITE_SIZE"]))
-      d = inst[name]
-      fetch = sum(d["FETCH_SIZE"]) / max(1, len(d["FETCH_SIZE"]))
-      write = sum(d["WRITE_SIZE"]) / max(1, len(d["WRITE_SIZE"]))
+      count = {n: max(len(v["FETCH_SIZE"]), len(v["WRITE_SIZE"])) for n, v in inst.items()}
+      top = max(count.values())
+      # (the probe round may launch an instance once more than the timed steps do)
+      timed = sorted(n for n in inst if count[n] >= 0.75 * top)
+      fetch = sum(mean(inst[n]["FETCH_SIZE"]) for n in timed)
+      write = sum(mean(inst[n]["WRITE_SIZE"]) for n in timed)
       m = mults[key]
-      out[key] = {"kernel": name, "FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write, "dispatches": len(d["FETCH_SIZE"]),
+      out[key] = {"kernel": timed, "FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write, "dispatches": top,
                   "fetch_raw_bytes": fetch * 1024.0, "write_raw_bytes": write * 1024.0,
                   "fetch_multiplier": m, "hbm_bytes_corrected": (m * fetch + write) * 1024.0,
-                  "other_instances": {n: {"dispatches": len(v["FETCH_SIZE"]),
-                                          "fetch_raw_bytes": sum(v["FETCH_SIZE"]) / max(1, len(v["FETCH_SIZE"])) * 1024.0,
-                                          "write_raw_bytes": sum(v["WRITE_SIZE"]) / max(1, len(v["WRITE_SIZE"])) * 1024.0}
-                                      for n, v in inst.items() if n != name}}
+                  "other_instances": {n: {"dispatches": count[n],
+                                          "fetch_raw_bytes": mean(v["FETCH_SIZE"]) * 1024.0,
+                                          "write_raw_bytes": mean(v["WRITE_SIZE"]) * 1024.0}
+                                      for n, v in inst.items() if n not in timed}}
     out["workload"] = w
     out["command"] = "tools/profile_workloads.sh <out> %s (bench.py --workload %s)" % (w, w)
     with open(os.path.join(dst, "traffic_%s.json" % w), "w") as fh:
