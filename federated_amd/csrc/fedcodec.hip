@@ -3684,7 +3684,10 @@ __global__ __launch_bounds__(64) void k_idx_scan(IdxArgs a) {
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_idx_emit(IdxArgs a) {
+#ifndef FC_IDX_EMIT_WPE
+#define FC_IDX_EMIT_WPE 4  // 6 or 8 (64-80 VGPRs) spill in the parse: 56 / 50 ms vs 38.5 at the headline
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX_EMIT_WPE))) void k_idx_emit(IdxArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lut[kLutSize];
   idx_load_lut(lut);
   const int64_t lanes = (int64_t)a.nclients * a.nchunks;

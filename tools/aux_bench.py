@@ -61,3 +61,10 @@ timed("qsgd decode+ordered sum, int8 rows", lambda: codec.decode_accumulate_scal
                                                                               qmax=17), code_bytes + C * P * 3)
 timed("int32 sum decode, same codes", lambda: codec.decode_accumulate(qb, want_sum=False, out=qout, step=1.0),
       code_bytes + P * 4)
+# Server decode of bare TFC strings (VERDICT r03 "next" 2): the decoder index rebuilt from the code bytes
+# alone (fc_build_index), then the same decode -- against the decode with the encoder's index above.
+nbq = np.asarray(qb.nbytes(), np.int64)
+nbt = torch.from_numpy(nbq).to(dev)
+timed("fc_build_index, same codes (bare strings)",
+      lambda: codec.index_codes(qb, nbt, int(nbq.max()), quarters=codec.quarter_index_wanted(C), check=False),
+      code_bytes)
