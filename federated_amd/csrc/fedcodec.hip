@@ -3275,6 +3275,15 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
 // ---------------------------------------------------------------------------
 constexpr int kIdxChunkBits = 4096;
 constexpr int64_t kIdxFail = -1;  // "the parse failed" (a guessed start, or past the stream's end)
+// Checkpoints of the guessed parse: at the first code start at or after every
+// kIdxCkBits bits of the chunk, (bits from the chunk start [12:0], runs so far
+// [63:13]).  A checkpoint at or after the point where the true parse meets the
+// guessed one is a true code start, and its last nonzero follows from the chunk's
+// true runs, so k_idx_emit parses from the checkpoint before each unit boundary
+// instead of the whole chunk.
+constexpr int kIdxCk = 7;
+constexpr int kIdxCkBits = kIdxChunkBits / (kIdxCk + 1);
+constexpr uint64_t kCkNone = ~0ull;
 
 struct IdxArgs {
   const uint8_t* stream_buf;
@@ -3288,6 +3297,8 @@ struct IdxArgs {
   int64_t* n1;      //               its sum of runs
   int64_t* x2;      //               true exit bit
   int64_t* n2;      //               true sum of runs, then (k_idx_scan) the last nonzero before the chunk
+  int64_t* xm;      //               where the true parse meets the guessed one (kIdxFail: it does not)
+  uint64_t* ck;     // [kIdxCk][C * nchunks]: the guessed parse's checkpoints (kCkNone: none)
   int32_t* ended;   // [nclients]
   uint64_t* idx;
   uint64_t* idxq;   // nullable
@@ -3366,6 +3377,7 @@ __device__ __forceinline__ uint32_t idx_code(IdxReader& r) {
 
 struct IdxLock {
   int64_t x, n;
+  int64_t m;  // (idx_lockstep) the meeting bit, kIdxFail if none
 };
 
 __device__ __forceinline__ const uint32_t* idx_words(const IdxArgs& a, int64_t c) {
@@ -3401,7 +3413,8 @@ struct IdxEnd {
 };
 template <bool EMIT>
 __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const uint32_t* lut, int64_t start,
-                                             int64_t stop, int64_t L, IdxEnd* end) {
+                                             int64_t stop, int64_t L, IdxEnd* end, uint64_t* ckp = nullptr,
+                                             int64_t ckst = 0, int64_t u_stop = INT64_MAX) {
   const int64_t nbits = 8 * a.nbytes[c];
   const uint8_t* base = a.stream_buf + a.stream_off[c];
   const int64_t cap = (a.nbytes[c] + 15) & ~15LL;  // readable: the 16-byte block holding the end
@@ -3433,7 +3446,12 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
   int32_t fill = restart(0);
   uint32_t it = 0;
   bool failed = false;
+  int nk = 0;  // (!EMIT, ckp) checkpoints recorded
   while (cons < lim) {
+    if (!EMIT && ckp && nk < kIdxCk && cons >= (nk + 1) * kIdxCkBits) {  // a code start: checkpoint
+      ckp[nk * ckst] = (uint64_t)cons | ((uint64_t)(nsum + (acc4 >> 2)) << 13);
+      ++nk;
+    }
     if ((++it & (kDecBatch - 1)) == 0) r.batch();
     const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
     const uint32_t Ls = e >> 26;
@@ -3514,6 +3532,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
         for (; u < nu && (u << gs) <= nz; ++u) idx_put(a, c, u, en);
         L = nz;
         room4 = room_of(L);
+        if (u > u_stop) break;  // the entries asked for are written
       } else {
         nsum += d;
       }
@@ -3525,6 +3544,8 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
       fill += 32;
     }
   }
+  if (!EMIT && ckp)
+    for (; nk < kIdxCk; ++nk) ckp[nk * ckst] = kCkNone;
   if (failed) return {kIdxFail, nsum};
   if (EMIT) {
     L += acc4 >> 2;
@@ -3554,7 +3575,11 @@ __global__ __launch_bounds__(kThreads) void k_idx_spec(IdxArgs a) {
     const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
     const int64_t cb = j * kIdxChunkBits;
     IdxLock r{kIdxFail, 0};
-    if (cb < 8 * a.nbytes[c]) r = idx_parse<false>(a, c, lut, cb, cb + kIdxChunkBits, 0, nullptr);
+    if (cb < 8 * a.nbytes[c]) {
+      r = idx_parse<false>(a, c, lut, cb, cb + kIdxChunkBits, 0, nullptr, a.ck + g, lanes);
+    } else {
+      for (int k = 0; k < kIdxCk; ++k) a.ck[k * lanes + g] = kCkNone;
+    }
     a.x1[g] = r.x;
     a.n1[g] = r.n;
   }
@@ -3572,7 +3597,7 @@ __device__ __noinline__ IdxLock idx_lockstep(const uint32_t* w, int64_t nbits, i
   int64_t pa = cb, pb = s, na = 0, nb = 0;
   bool adone = false;
   for (;;) {
-    if (pa == pb) return {x1, n1 - na + nb};
+    if (pa == pb) return {x1, n1 - na + nb, pa};
     if (pa < pb && !adone) {
       if (pa >= ce) {
         adone = true;  // A left the chunk at x1
@@ -3587,9 +3612,9 @@ __device__ __noinline__ IdxLock idx_lockstep(const uint32_t* w, int64_t nbits, i
       }
       continue;
     }
-    if (pb >= ce) return {pb, nb};
+    if (pb >= ce) return {pb, nb, kIdxFail};
     const uint32_t d = idx_code(B);
-    if (!d) return {kIdxFail, nb};
+    if (!d) return {kIdxFail, nb, kIdxFail};
     nb += d;
     pb = B.pos;
   }
@@ -3601,15 +3626,16 @@ __global__ __launch_bounds__(kThreads) void k_idx_sync(IdxArgs a) {
   const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
   const int64_t nbits = 8 * a.nbytes[c];
   const int64_t cb = j * kIdxChunkBits;
-  IdxLock r{kIdxFail, 0};
+  IdxLock r{kIdxFail, 0, kIdxFail};
   if (j == 0) {
-    r = {a.x1[g], a.n1[g]};  // chunk 0 starts at bit 0: its parse is the true one
+    r = {a.x1[g], a.n1[g], 0};  // chunk 0 starts at bit 0: its parse is the true one
   } else if (cb < nbits) {
     const int64_t s = a.x1[g - 1];
     if (s != kIdxFail) r = idx_lockstep(idx_words(a, c), nbits, cb, cb + kIdxChunkBits, s, a.x1[g], a.n1[g]);
   }
   a.x2[g] = r.x;
   a.n2[g] = r.n;
+  a.xm[g] = r.m;
 }
 
 __device__ __forceinline__ int64_t rfl64(int64_t v) {
@@ -3647,7 +3673,7 @@ __global__ __launch_bounds__(64) void k_idx_fix(IdxArgs a) {
     const int k = __builtin_ctzll(m);
     const int64_t jk = j0 + k;
     const int64_t s = k == 0 ? carried : x2[jk - 1];
-    IdxLock r{kIdxFail, 0};
+    IdxLock r{kIdxFail, 0, kIdxFail};
     if (lane == 0 && s != kIdxFail) {
       const int64_t cb = jk * kIdxChunkBits;
       r = idx_lockstep(w, nbits, cb, cb + kIdxChunkBits, s, x1[jk], n1[jk]);
@@ -3655,6 +3681,7 @@ __global__ __launch_bounds__(64) void k_idx_fix(IdxArgs a) {
     if (lane == 0) {
       x2[jk] = r.x;
       n2[jk] = r.n;
+      a.xm[c * a.nchunks + jk] = r.m;
     }
     carried = rfl64(r.x);
     j0 = jk + 1;
@@ -3691,6 +3718,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX
   __shared__ __attribute__((aligned(16))) uint32_t lut[kLutSize];
   idx_load_lut(lut);
   const int64_t lanes = (int64_t)a.nclients * a.nchunks;
+  const int gs = a.idxq ? 8 : 10;  // unit: quarter tile or tile
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < lanes; g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
     const int64_t nbits = 8 * a.nbytes[c];
@@ -3701,14 +3729,54 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX
     const int64_t L = a.n2[g];    // the last nonzero before the chunk's first code
     if (L >= a.P) continue;       // (past the trailing run of a code with bytes after it)
     IdxEnd end{-1, -1, false};
-    idx_parse<true>(a, c, lut, s, ce, L, &end);
-    if (end.bad) {
-      atomicOr(a.err, 1);
-    } else if (end.bend >= 0) {
-      if ((end.total + 7) / 8 != a.nbytes[c]) atomicOr(a.err, 1);  // bytes after the code, or a short final byte
-    } else if (ce >= nbits) {
-      atomicOr(a.err, 1);  // the code ends before its elements do
+    // checkpoints: a chunk two or more before the code's last, whose true parse met the
+    // guessed one and whose codes stay short of the last element
+    const int64_t m = a.xm[g];
+    bool ckd = kIdxCk > 0 && j + 1 < (nbits - 1) / kIdxChunkBits && a.x2[g] != kIdxFail && m != kIdxFail;
+    const int64_t Lnext = ckd ? a.n2[g + 1] : 0;  // the last nonzero of the chunk's last code
+    ckd = ckd && Lnext >= L && Lnext < a.P - 1;
+    if (!ckd) {  // the whole chunk, ends and all
+      idx_parse<true>(a, c, lut, s, ce, L, &end);
+      if (end.bad) {
+        atomicOr(a.err, 1);
+      } else if (end.bend >= 0) {
+        if ((end.total + 7) / 8 != a.nbytes[c]) atomicOr(a.err, 1);  // bytes after the code, or a short final byte
+      } else if (ce >= nbits) {
+        atomicOr(a.err, 1);  // the code ends before its elements do
+      }
+      continue;
     }
+    // the units whose first element lies in (L, Lnext]: for each, a parse from the latest
+    // true code start before it -- the last parse's end, or a checkpoint past the meeting
+    const int64_t adj = Lnext - a.n1[g];  // checkpoint runs (guessed parse) -> last nonzero
+    int64_t u = (L + ((int64_t)1 << gs)) >> gs;
+    const int64_t ulast = Lnext >> gs;
+    int64_t cp = s, cl = L;
+    bool bad = false;
+    while (u <= ulast) {
+      const int64_t bound = u << gs;
+      int64_t ps = cp, pl = cl;
+      for (int k = 0; k < kIdxCk; ++k) {
+        const uint64_t e = a.ck[k * lanes + g];
+        if (e == kCkNone) break;
+        const int64_t pos = cb + (int64_t)(e & 0x1FFFu);
+        const int64_t lk = adj + (int64_t)(e >> 13);
+        if (lk >= bound) break;
+        if (pos >= m && pos > ps) {
+          ps = pos;
+          pl = lk;
+        }
+      }
+      const IdxLock r = idx_parse<true>(a, c, lut, ps, ce, pl, &end, nullptr, 0, u);
+      if (end.bad || end.bend >= 0 || r.n < bound) {  // (a chunk before the last holds no end)
+        bad = true;
+        break;
+      }
+      cp = r.x;
+      cl = r.n;
+      u = (cl + ((int64_t)1 << gs)) >> gs;
+    }
+    if (bad) atomicOr(a.err, 1);
   }
 }
 
@@ -5332,10 +5400,11 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   return check_launch("k_decode");
 }
 
-// fc_build_index workspace: x1 | n1 | x2 | n2 (int64 [nclients][nchunks] each) | ended (int32 [nclients]).
+// fc_build_index workspace: x1 | n1 | x2 | n2 | xm (int64 [nclients][nchunks] each) | ck (u64
+// [kIdxCk][nclients * nchunks]) | ended (int32 [nclients]).
 int64_t idx_nchunks(int64_t max_bytes) { return std::max<int64_t>(1, (8 * max_bytes + kIdxChunkBits - 1) / kIdxChunkBits); }
 int64_t idx_workspace_bytes(int32_t n, int64_t max_bytes) {
-  return 4 * 8 * (int64_t)n * idx_nchunks(max_bytes) + ((4 * (int64_t)n + 255) & ~255LL);
+  return (5 + kIdxCk) * 8 * (int64_t)n * idx_nchunks(max_bytes) + ((4 * (int64_t)n + 255) & ~255LL);
 }
 
 int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* nbytes, int32_t nclients,
@@ -5361,7 +5430,9 @@ int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int6
   a.n1 = w + lanes;
   a.x2 = w + 2 * lanes;
   a.n2 = w + 3 * lanes;
-  a.ended = (int32_t*)(w + 4 * lanes);
+  a.xm = w + 4 * lanes;
+  a.ck = (uint64_t*)(w + 5 * lanes);
+  a.ended = (int32_t*)(w + (5 + kIdxCk) * lanes);
   a.idx = idx;
   a.idxq = idxq;
   a.total_bits = total_bits;
