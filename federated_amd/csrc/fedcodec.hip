@@ -3041,6 +3041,10 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       if (L <= 32u) {
         r.win <<= L;
       } else {  // a code longer than 32 bits (or a malformed one)
+        // land any batch-point load first: the registers it writes are free to the
+        // compiler from here on (r.init below issues a new load into them), and
+        // slow_code is a call whose temporaries may be those registers
+        r.wait_nxt();
         const uint64_t pos = b0 + (uint64_t)cons;
         const CodeVal cv = slow_code(base, cap, pos);
         if (cv.L == 0) {
@@ -3282,6 +3286,9 @@ constexpr int64_t kIdxFail = -1;  // "the parse failed" (a guessed start, or pas
 // true runs, so k_idx_emit parses from the checkpoint before each unit boundary
 // instead of the whole chunk.
 constexpr int kIdxCk = 7;
+#ifndef FC_IDX_ASYNC
+#define FC_IDX_ASYNC 0
+#endif
 constexpr int kIdxCkBits = kIdxChunkBits / (kIdxCk + 1);
 constexpr uint64_t kCkNone = ~0ull;
 
@@ -3437,7 +3444,9 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
   // bits of the code from `start` on: a table / window code must end inside them (so
   // every path accepts exactly the codes the IdxReader does)
   const int32_t avail = (int32_t)min<int64_t>(nbits - start, (int64_t)lim + 8192);
-  SegReaderT<false> r;
+  // (FC_IDX_ASYNC: the guessed parse on the decoder's untracked batch-point loads --
+  // tools/audit_async_loads.py checks that no destination register is touched early)
+  SegReaderT<!EMIT && FC_IDX_ASYNC> r;
   auto restart = [&](int32_t cons) {
     r.init(base, cap, (uint64_t)(start + cons), (int32_t)min<int64_t>(nbits - start - cons, lim - cons + 8192));
     return cons + r.nwin;
@@ -3495,6 +3504,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
         cons += (int32_t)Lw;
         took = true;
       } else {
+        r.wait_nxt();  // (async) as in decode_segment's slow path: land the batch-point load first
         IdxReader ir;
         ir.init(w, nbits, p);
         d = idx_gamma(ir);
@@ -3544,6 +3554,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
       fill += 32;
     }
   }
+  r.wait_nxt();  // (async) the last batch-point load lands before its registers are reused
   if (!EMIT && ckp)
     for (; nk < kIdxCk; ++nk) ckp[nk * ckst] = kCkNone;
   if (failed) return {kIdxFail, nsum};

@@ -1,6 +1,6 @@
 """CPU guard (no GPU): the decoder's untracked inline-asm loads keep their destination
-registers untouched until their asm wait (tools/audit_async_loads.py; the fault class
-that took down a GPU run in round 4)."""
+registers free of clobbers, copies and calls on every path until a vmcnt(0) wait
+(tools/audit_async_loads.py; the fault class that took down a GPU run in round 4)."""
 import os
 import sys
 
