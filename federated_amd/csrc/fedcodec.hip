@@ -2945,7 +2945,10 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       if ((uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(ex)) atomicAdd(&g_stamps[15], 1ull);
     }
 #endif
-    if ((++it & (kDecBatch - 1)) == 0) r.batch();  // every active lane is on the same iteration
+    // every active lane is on the same iteration: a wave-uniform count (the scalar unit
+    // keeps it, not three VALU per iteration where the loop's exit is divergent)
+    it = __builtin_amdgcn_readfirstlane(it + 1u);
+    if ((it & (kDecBatch - 1)) == 0) r.batch();
 #if FC_DEC_ABL & 16  // diagnostics: 12 extra independent VALU per iteration (is the loop issue-bound?)
     {
       uint32_t p0 = it, p1 = it + 1, p2 = it + 2, p3 = it + 3;
@@ -3461,7 +3464,8 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
       ckp[nk * ckst] = (uint64_t)cons | ((uint64_t)(nsum + (acc4 >> 2)) << 13);
       ++nk;
     }
-    if ((++it & (kDecBatch - 1)) == 0) r.batch();
+    it = __builtin_amdgcn_readfirstlane(it + 1u);
+    if ((it & (kDecBatch - 1)) == 0) r.batch();
     const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
     const uint32_t Ls = e >> 26;
     const int32_t dd4 = (int32_t)((e & 0x7Fu) + ((e >> 7) & 0x7Fu));

@@ -12,3 +12,7 @@ for v in "$A" "$PWD/federated_amd/libfedcodec.so"; do
   echo "== $v"
   FEDCODEC_LIB=$v timeout -k 10 200 python3 tools/index_bench.py 2>&1 | grep -v amdgpu.ids || exit 2
 done
+for rep in 1 2; do
+  C=128 P=1048576 STEP=0.007874015748031496 SIGMA=0.25 ITERS=6 timeout -k 10 100 python3 tools/dec_bench.py 2>&1 | grep -v amdgpu.ids | tail -2
+  C=1024 ITERS=3 timeout -k 10 150 python3 tools/dec_bench.py 2>&1 | grep -v amdgpu.ids | tail -1
+done
