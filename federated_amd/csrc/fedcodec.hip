@@ -3470,7 +3470,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
     const uint32_t Ls = e >> 26;
     const int32_t dd4 = (int32_t)((e & 0x7Fu) + ((e >> 7) & 0x7Fu));
     const int32_t lend = min(lim, avail);  // a table step's codes must end inside both
-    if (Ls != 0u && cons + (int32_t)Ls <= lend && acc4 + dd4 < room4) {
+    if (Ls != 0u && cons + (int32_t)Ls <= lend && (!EMIT || acc4 + dd4 < room4)) {
       r.win <<= Ls;
       cons += (int32_t)Ls;
       acc4 += dd4;
@@ -3479,7 +3479,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
       const uint32_t e2 = lut[(uint32_t)(r.win >> (64 - kLutBits))];
       const uint32_t L2 = e2 >> 26;
       const int32_t d24 = (int32_t)((e2 & 0x7Fu) + ((e2 >> 7) & 0x7Fu));
-      if (L2 != 0u && cons + (int32_t)L2 <= lend && acc4 + d24 < room4) {
+      if (L2 != 0u && cons + (int32_t)L2 <= lend && (!EMIT || acc4 + d24 < room4)) {
         r.win <<= L2;
         cons += (int32_t)L2;
         acc4 += d24;
