@@ -283,6 +283,27 @@ def _stream_key(device, stream):
   return (torch.device(device).index or 0, s.cuda_stream)
 
 
+_WS_STREAMS = 8  # per-stream workspaces kept (least recently used dropped first)
+
+
+def _ws_slot(bufs, key, stream):
+  """The cached buffer of `key` (most recently used now), the least recently used
+  dropped past _WS_STREAMS; a buffer used on a side stream is recorded on it, so
+  the caching allocator does not hand it out again while that stream's work runs."""
+  buf = bufs.pop(key, None)
+  if buf is not None:
+    bufs[key] = buf
+  while len(bufs) > _WS_STREAMS:
+    bufs.pop(next(iter(bufs)))
+  return buf
+
+
+def _ws_use(buf, stream):
+  if stream is not None:
+    buf.record_stream(stream)
+  return buf
+
+
 class Workspace:
   """Grow-only device workspace for the encoder's look-back status array, one per
   stream: encodes on different streams may run at once and must not share the
@@ -295,12 +316,12 @@ class Workspace:
   def get(self, nclients, P, device, stream=None):
     need = int(_lib.load().fc_encode_workspace_bytes(int(nclients), int(P)))
     key = _stream_key(device, stream)
-    buf = self.bufs.get(key)
+    buf = _ws_slot(self.bufs, key, stream)
     if buf is None or buf.numel() < need:
       self.bufs[key] = None
       buf = torch.empty(_round_up(need, 256), dtype=torch.uint8, device=device)
       self.bufs[key] = buf
-    return buf
+    return _ws_use(buf, stream)
 
 
 _WS = Workspace()
@@ -318,11 +339,12 @@ class SegWorkspace:
     if need < 0:
       return None
     key = _stream_key(device, stream)
-    buf = self.bufs.get(key)
+    buf = _ws_slot(self.bufs, key, stream)
     if buf is None or buf.numel() < need + 256:
       self.bufs[key] = None
       buf = torch.empty(_round_up(need + 256, 256), dtype=torch.uint8, device=device)
       self.bufs[key] = buf
+    _ws_use(buf, stream)
     off = (-buf.data_ptr()) % 256
     return buf[off:off + need]
 
