@@ -2620,9 +2620,6 @@ __device__ __noinline__ CodeVal slow_code(const uint8_t* base, int64_t cap, uint
 // 16-byte reads.  Loads are issued only at batch points the wave reaches
 // together every kDecBatch iterations, so the wave's in-order memory counter
 // does not make a lane wait for loads other lanes issued an iteration ago.
-#ifndef FC_DEC_SEL_REFILL
-#define FC_DEC_SEL_REFILL 0  // window refill by selects instead of a branch (A/B knob)
-#endif
 #ifndef FC_DEC_ABL
 #define FC_DEC_ABL 0  // decoder ablation bits (diagnostics only): 1 sums one bank per lane, 2 no sums, 8 eight clients' streams for all lanes
 #endif
@@ -3069,24 +3066,11 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       acc_add_at<PLANE>(relb, v, ptile, hib, err);
       cons += (int32_t)L;
     }
-#if FC_DEC_SEL_REFILL
-    {  // branch-free refill: selects instead of an exec-masked block
-      const bool need = fill - cons <= 32;
-      const uint32_t w = need ? (uint32_t)(r.rh >> 32) : 0u;
-      r.win |= (uint64_t)w << ((uint32_t)(32 - (fill - cons)) & 63u);
-      r.rh = need ? ((r.rh << 32) | (r.rl >> 32)) : r.rh;
-      r.rl = need ? (r.rl << 32) : r.rl;
-      r.rb -= need ? 32 : 0;
-      fill += need ? 32 : 0;
-      if (r.rb == 0) r.take_block();
-    }
-#else
     if (fill - cons <= 32) {  // (the blocks are zero past the segment end)
       const uint32_t w = r.pop32();
       r.win |= (uint64_t)w << (32 - (fill - cons));
       fill += 32;
     }
-#endif
     }
     if (stop) break;
   }
