@@ -3734,28 +3734,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX
     bool ckd = kIdxCk > 0 && j + 1 < (nbits - 1) / kIdxChunkBits && a.x2[g] != kIdxFail && m != kIdxFail;
     const int64_t Lnext = ckd ? a.n2[g + 1] : 0;  // the last nonzero of the chunk's last code
     ckd = ckd && Lnext >= L && Lnext < a.P - 1;
-    if (!ckd) {  // the whole chunk, ends and all
-      idx_parse<true>(a, c, lut, s, ce, L, &end);
-      if (end.bad) {
-        atomicOr(a.err, 1);
-      } else if (end.bend >= 0) {
-        if ((end.total + 7) / 8 != a.nbytes[c]) atomicOr(a.err, 1);  // bytes after the code, or a short final byte
-      } else if (ce >= nbits) {
-        atomicOr(a.err, 1);  // the code ends before its elements do
-      }
-      continue;
-    }
-    // the units whose first element lies in (L, Lnext]: for each, a parse from the latest
-    // true code start before it -- the last parse's end, or a checkpoint past the meeting
+    // !ckd: the whole chunk, ends and all (one parse).  ckd: the units whose first element
+    // lies in (L, Lnext], each by a parse from the latest true code start before it -- the
+    // last parse's end, or a checkpoint past the meeting.  One parse call site either way.
     const int64_t adj = Lnext - a.n1[g];  // checkpoint runs (guessed parse) -> last nonzero
     int64_t u = (L + ((int64_t)1 << gs)) >> gs;
-    const int64_t ulast = Lnext >> gs;
+    const int64_t ulast = ckd ? Lnext >> gs : u;
     int64_t cp = s, cl = L;
     bool bad = false;
     while (u <= ulast) {
       const int64_t bound = u << gs;
       int64_t ps = cp, pl = cl;
-      for (int k = 0; k < kIdxCk; ++k) {
+      for (int k = 0; ckd && k < kIdxCk; ++k) {
         const uint64_t e = a.ck[k * lanes + g];
         if (e == kCkNone) break;
         const int64_t pos = cb + (int64_t)(e & 0x1FFFu);
@@ -3766,7 +3756,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX
           pl = lk;
         }
       }
-      const IdxLock r = idx_parse<true>(a, c, lut, ps, ce, pl, &end, nullptr, 0, u);
+      const IdxLock r = idx_parse<true>(a, c, lut, ps, ce, pl, &end, nullptr, 0, ckd ? u : INT64_MAX);
+      if (!ckd) {
+        if (end.bad) {
+          bad = true;
+        } else if (end.bend >= 0) {
+          bad = (end.total + 7) / 8 != a.nbytes[c];  // bytes after the code, or a short final byte
+        } else {
+          bad = ce >= nbits;  // the code ends before its elements do
+        }
+        break;
+      }
       if (end.bad || end.bend >= 0 || r.n < bound) {  // (a chunk before the last holds no end)
         bad = true;
         break;
