@@ -3243,7 +3243,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
 // (G = 1024, or 256 with the quarter index), entry T = the bit where the trailing
 // zero-run code starts (or the stream's end).
 //
-// A prefix code is parsed serially, so each lane parses its own kIdxChunkBits
+// A prefix code is parsed serially, so each lane parses its own chunk (a.chunk bits)
 // of a client's code from a GUESSED start -- the chunk's first bit taken as a
 // code start -- and records where its parse leaves the chunk (the first code
 // start at or after the chunk's end) and the zero runs it summed.  Run-length
@@ -3264,19 +3264,21 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
 //                trailing run, the bit count and the byte length
 //   k_idx_check  a client whose code never ended is malformed
 // ---------------------------------------------------------------------------
-constexpr int kIdxChunkBits = 4096;
+// bits per chunk lane, chosen per launch (idx_chunk_bits): 2048, 4096 or 8192 (<= 8192:
+// 13-bit checkpoint positions)
+constexpr int kIdxChunkMax = 8192;
 constexpr int64_t kIdxFail = -1;  // "the parse failed" (a guessed start, or past the stream's end)
 // Checkpoints of the guessed parse: at the first code start at or after every
-// kIdxCkBits bits of the chunk, (bits from the chunk start [12:0], runs so far
+// a.ckb bits of the chunk, (bits from the chunk start [12:0], runs so far
 // [63:13]).  A checkpoint at or after the point where the true parse meets the
 // guessed one is a true code start, and its last nonzero follows from the chunk's
 // true runs, so k_idx_emit parses from the checkpoint before each unit boundary
 // instead of the whole chunk.
-constexpr int kIdxCk = 7;
+// per chunk: nck = min(15, chunk / 256 - 1) checkpoints, chunk / (nck + 1) bits apart
+inline int32_t idx_nck(int32_t chunk) { return std::min(15, chunk / 256 - 1); }
 #ifndef FC_IDX_ASYNC
 #define FC_IDX_ASYNC 0
 #endif
-constexpr int kIdxCkBits = kIdxChunkBits / (kIdxCk + 1);
 constexpr uint64_t kCkNone = ~0ull;
 
 struct IdxArgs {
@@ -3292,7 +3294,10 @@ struct IdxArgs {
   int64_t* x2;      //               true exit bit
   int64_t* n2;      //               true sum of runs, then (k_idx_scan) the last nonzero before the chunk
   int64_t* xm;      //               where the true parse meets the guessed one (kIdxFail: it does not)
-  uint64_t* ck;     // [kIdxCk][C * nchunks]: the guessed parse's checkpoints (kCkNone: none)
+  uint64_t* ck;     // [nck][C * nchunks]: the guessed parse's checkpoints (kCkNone: none)
+  int32_t chunk;    // bits per chunk lane
+  int32_t nck;      // checkpoints per chunk (idx_nck)
+  int32_t ckb;      // their spacing: chunk / (nck + 1) bits
   int32_t* ended;   // [nclients]
   uint64_t* idx;
   uint64_t* idxq;   // nullable
@@ -3444,7 +3449,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
   bool failed = false;
   int nk = 0;  // (!EMIT, ckp) checkpoints recorded
   while (cons < lim) {
-    if (!EMIT && ckp && nk < kIdxCk && cons >= (nk + 1) * kIdxCkBits) {  // a code start: checkpoint
+    if (!EMIT && ckp && nk < a.nck && cons >= (nk + 1) * a.ckb) {  // a code start: checkpoint
       ckp[nk * ckst] = (uint64_t)cons | ((uint64_t)(nsum + (acc4 >> 2)) << 13);
       ++nk;
     }
@@ -3544,7 +3549,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
   }
   r.wait_nxt();  // (async) the last batch-point load lands before its registers are reused
   if (!EMIT && ckp)
-    for (; nk < kIdxCk; ++nk) ckp[nk * ckst] = kCkNone;
+    for (; nk < a.nck; ++nk) ckp[nk * ckst] = kCkNone;
   if (failed) return {kIdxFail, nsum};
   if (EMIT) {
     L += acc4 >> 2;
@@ -3572,12 +3577,12 @@ __global__ __launch_bounds__(kThreads) void k_idx_spec(IdxArgs a) {
   const int64_t lanes = (int64_t)a.nclients * a.nchunks;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < lanes; g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
-    const int64_t cb = j * kIdxChunkBits;
+    const int64_t cb = j * a.chunk;
     IdxLock r{kIdxFail, 0};
     if (cb < 8 * a.nbytes[c]) {
-      r = idx_parse<false>(a, c, lut, cb, cb + kIdxChunkBits, 0, nullptr, a.ck + g, lanes);
+      r = idx_parse<false>(a, c, lut, cb, cb + a.chunk, 0, nullptr, a.ck + g, lanes);
     } else {
-      for (int k = 0; k < kIdxCk; ++k) a.ck[k * lanes + g] = kCkNone;
+      for (int k = 0; k < a.nck; ++k) a.ck[k * lanes + g] = kCkNone;
     }
     a.x1[g] = r.x;
     a.n1[g] = r.n;
@@ -3624,13 +3629,13 @@ __global__ __launch_bounds__(kThreads) void k_idx_sync(IdxArgs a) {
   if (g >= (int64_t)a.nclients * a.nchunks) return;
   const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
   const int64_t nbits = 8 * a.nbytes[c];
-  const int64_t cb = j * kIdxChunkBits;
+  const int64_t cb = j * a.chunk;
   IdxLock r{kIdxFail, 0, kIdxFail};
   if (j == 0) {
     r = {a.x1[g], a.n1[g], 0};  // chunk 0 starts at bit 0: its parse is the true one
   } else if (cb < nbits) {
     const int64_t s = a.x1[g - 1];
-    if (s != kIdxFail) r = idx_lockstep(idx_words(a, c), nbits, cb, cb + kIdxChunkBits, s, a.x1[g], a.n1[g]);
+    if (s != kIdxFail) r = idx_lockstep(idx_words(a, c), nbits, cb, cb + a.chunk, s, a.x1[g], a.n1[g]);
   }
   a.x2[g] = r.x;
   a.n2[g] = r.n;
@@ -3650,7 +3655,7 @@ __global__ __launch_bounds__(64) void k_idx_fix(IdxArgs a) {
   const int64_t c = blockIdx.x;
   const int lane = threadIdx.x;
   const int64_t nbits = 8 * a.nbytes[c];
-  const int64_t nch = min<int64_t>(a.nchunks, (nbits + kIdxChunkBits - 1) / kIdxChunkBits);
+  const int64_t nch = min<int64_t>(a.nchunks, (nbits + a.chunk - 1) / a.chunk);
   if (nch <= 1) return;
   const int64_t* x1 = a.x1 + c * a.nchunks;
   const int64_t* n1 = a.n1 + c * a.nchunks;
@@ -3674,8 +3679,8 @@ __global__ __launch_bounds__(64) void k_idx_fix(IdxArgs a) {
     const int64_t s = k == 0 ? carried : x2[jk - 1];
     IdxLock r{kIdxFail, 0, kIdxFail};
     if (lane == 0 && s != kIdxFail) {
-      const int64_t cb = jk * kIdxChunkBits;
-      r = idx_lockstep(w, nbits, cb, cb + kIdxChunkBits, s, x1[jk], n1[jk]);
+      const int64_t cb = jk * a.chunk;
+      r = idx_lockstep(w, nbits, cb, cb + a.chunk, s, x1[jk], n1[jk]);
     }
     if (lane == 0) {
       x2[jk] = r.x;
@@ -3693,7 +3698,7 @@ __global__ __launch_bounds__(64) void k_idx_scan(IdxArgs a) {
   const int64_t c = blockIdx.x;
   const int lane = threadIdx.x;
   const int64_t nbits = 8 * a.nbytes[c];
-  const int64_t nch = min<int64_t>(a.nchunks, (nbits + kIdxChunkBits - 1) / kIdxChunkBits);
+  const int64_t nch = min<int64_t>(a.nchunks, (nbits + a.chunk - 1) / a.chunk);
   int64_t* n2 = a.n2 + c * a.nchunks;
   int64_t run = -1;
   for (int64_t j0 = 0; j0 < nch; j0 += 64) {
@@ -3721,7 +3726,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < lanes; g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t c = g / a.nchunks, j = g - c * a.nchunks;
     const int64_t nbits = 8 * a.nbytes[c];
-    const int64_t cb = j * kIdxChunkBits, ce = cb + kIdxChunkBits;
+    const int64_t cb = j * a.chunk, ce = cb + a.chunk;
     if (cb >= nbits) continue;  // (an empty code never ends: k_idx_check)
     const int64_t s = j == 0 ? 0 : a.x2[g - 1];
     if (s == kIdxFail) continue;  // past the code's end
@@ -3731,7 +3736,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX
     // checkpoints: a chunk two or more before the code's last, whose true parse met the
     // guessed one and whose codes stay short of the last element
     const int64_t m = a.xm[g];
-    bool ckd = kIdxCk > 0 && j + 1 < (nbits - 1) / kIdxChunkBits && a.x2[g] != kIdxFail && m != kIdxFail;
+    bool ckd = a.nck > 0 && j + 1 < (nbits - 1) / a.chunk && a.x2[g] != kIdxFail && m != kIdxFail;
     const int64_t Lnext = ckd ? a.n2[g + 1] : 0;  // the last nonzero of the chunk's last code
     ckd = ckd && Lnext >= L && Lnext < a.P - 1;
     // !ckd: the whole chunk, ends and all (one parse).  ckd: the units whose first element
@@ -3745,7 +3750,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX
     while (u <= ulast) {
       const int64_t bound = u << gs;
       int64_t ps = cp, pl = cl;
-      for (int k = 0; ckd && k < kIdxCk; ++k) {
+      for (int k = 0; ckd && k < a.nck; ++k) {
         const uint64_t e = a.ck[k * lanes + g];
         if (e == kCkNone) break;
         const int64_t pos = cb + (int64_t)(e & 0x1FFFu);
@@ -5400,10 +5405,28 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
 }
 
 // fc_build_index workspace: x1 | n1 | x2 | n2 | xm (int64 [nclients][nchunks] each) | ck (u64
-// [kIdxCk][nclients * nchunks]) | ended (int32 [nclients]).
-int64_t idx_nchunks(int64_t max_bytes) { return std::max<int64_t>(1, (8 * max_bytes + kIdxChunkBits - 1) / kIdxChunkBits); }
+// [nck][nclients * nchunks]) | ended (int32 [nclients]).
+// Chunk size: the largest of 8192 / 4096 / 2048 bits that still gives about 600 K chunk
+// lanes (a full chip's parse lanes about once over) -- longer chunks spend less per lane
+// on the guess, the lockstep and the checkpoints, shorter ones fill the chip (measured:
+// 1024 x 25 M 22.4 / 24.0 / 31.0 ms at 8192 / 4096 / 2048; config 2 1.22 / 0.93 / 0.91; config 3
+// 1.14 / 1.01 / 1.20).
+int32_t idx_chunk_bits(int32_t n, int64_t max_bytes) {
+  int32_t cb = kIdxChunkMax;
+  while (cb > 2048 && (int64_t)n * ((8 * max_bytes + cb - 1) / cb) < 600000) cb /= 2;
+  if (const char* e = getenv("FEDCODEC_IDX_CHUNK")) {  // test knob
+    const int v = atoi(e);
+    if (v == 2048 || v == 4096 || v == 8192) cb = v;
+  }
+  return cb;
+}
+int64_t idx_nchunks(int32_t n, int64_t max_bytes) {
+  const int64_t cb = idx_chunk_bits(n, max_bytes);
+  return std::max<int64_t>(1, (8 * max_bytes + cb - 1) / cb);
+}
 int64_t idx_workspace_bytes(int32_t n, int64_t max_bytes) {
-  return (5 + kIdxCk) * 8 * (int64_t)n * idx_nchunks(max_bytes) + ((4 * (int64_t)n + 255) & ~255LL);
+  const int64_t nck = idx_nck(idx_chunk_bits(n, max_bytes));
+  return (5 + nck) * 8 * (int64_t)n * idx_nchunks(n, max_bytes) + ((4 * (int64_t)n + 255) & ~255LL);
 }
 
 int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* nbytes, int32_t nclients,
@@ -5422,7 +5445,10 @@ int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int6
   a.nclients = nclients;
   a.P = P;
   a.T = (int32_t)tiles_for(P);
-  a.nchunks = idx_nchunks(max_bytes);
+  a.chunk = idx_chunk_bits(nclients, max_bytes);
+  a.nck = idx_nck(a.chunk);
+  a.ckb = a.chunk / (a.nck + 1);
+  a.nchunks = idx_nchunks(nclients, max_bytes);
   const int64_t lanes = (int64_t)nclients * a.nchunks;
   int64_t* w = (int64_t*)workspace;
   a.x1 = w;
@@ -5431,7 +5457,7 @@ int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int6
   a.n2 = w + 3 * lanes;
   a.xm = w + 4 * lanes;
   a.ck = (uint64_t*)(w + 5 * lanes);
-  a.ended = (int32_t*)(w + (5 + kIdxCk) * lanes);
+  a.ended = (int32_t*)(w + (5 + (int64_t)a.nck) * lanes);
   a.idx = idx;
   a.idxq = idxq;
   a.total_bits = total_bits;

@@ -14,7 +14,8 @@ Checked here:
   * the rebuilt index (and quarter index) equal to the HIP encoder's, entry for
     entry, and the rebuilt bit lengths equal to the oracle's;
   * edge cases: P = 1, all-zero tensors (one trailing run code), no trailing run,
-    runs across many tiles, codes ending on a 4096-bit lane-chunk boundary, |q| =
+    runs across many tiles, codes ending on a lane-chunk boundary (2048-, 4096- and
+    8192-bit chunks), |q| =
     2^31 (INT_MIN), 63-bit magnitude codes, very sparse and very dense streams;
   * malformed codes rejected: truncated, a byte appended, bits flipped, an empty
     code, a code of another element count.
@@ -31,6 +32,17 @@ from oracle import quantize_utils as oq
 pytestmark = pytest.mark.gpu
 
 F32 = np.float32
+
+# fc_build_index picks 2048-, 4096- or 8192-bit chunk lanes by the batch's size; the
+# tests below run at each (FEDCODEC_IDX_CHUNK) -- small batches would otherwise all
+# take 2048-bit chunks
+CHUNKS = [2048, 4096, 8192]
+
+
+@pytest.fixture(params=CHUNKS, ids=lambda v: "chunk%d" % v)
+def chunk(request, monkeypatch):
+  monkeypatch.setenv("FEDCODEC_IDX_CHUNK", str(request.param))
+  return request.param
 
 
 def _oracle_codes(qs):
@@ -82,7 +94,7 @@ def test_headline_tensor_oracle_codes(gpu):
 
 
 @pytest.mark.parametrize("C,P,quarters", [(5, 70_001, False), (5, 70_001, True), (300, 9_000, False)])
-def test_rebuilt_index_equals_encoder_index(gpu, C, P, quarters):
+def test_rebuilt_index_equals_encoder_index(gpu, chunk, C, P, quarters):
   """The index rebuilt from the bytes equals the HIP encoder's own, entry for entry
   (quarter entries too), for mixed-density clients."""
   rng = np.random.default_rng(C + P)
@@ -136,7 +148,7 @@ def _edge_qs():
 
 
 @pytest.mark.parametrize("name", sorted(_edge_qs()))
-def test_edge_case_codes(gpu, name):
+def test_edge_case_codes(gpu, chunk, name):
   q = _edge_qs()[name]
   P = q.size
   code = ocodec.run_length_gamma_encode(q)[0]
@@ -149,9 +161,9 @@ def test_edge_case_codes(gpu, name):
     np.testing.assert_array_equal(s.cpu().numpy(), want)
 
 
-def test_chunk_boundary_sweep(gpu):
-  """Codes of every length around the 4096-bit lane chunks: a code start, a code's
-  middle and the trailing run landing on each boundary."""
+def test_chunk_boundary_sweep(gpu, chunk):
+  """Codes of every length around 4096 bits (a lane-chunk boundary at every chunk size):
+  a code start, a code's middle and the trailing run landing on each boundary."""
   rng = np.random.default_rng(5)
   codes, qs = [], []
   for extra in range(0, 40):
@@ -171,7 +183,7 @@ def _good_code(P=100_000, seed=1):
 
 
 @pytest.mark.parametrize("how", ["truncated", "appended", "empty", "other_P", "garbage"])
-def test_malformed_codes_rejected(gpu, how):
+def test_malformed_codes_rejected(gpu, chunk, how):
   q, code = _good_code()
   P = q.size
   if how == "truncated":

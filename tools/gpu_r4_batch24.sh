@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-4 GPU batch 24: per-launch index chunk size (2048 / 4096 / 8192 bits) -- bare-decode tests at every
+# size, then the rebuild timing
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+timeout -k 10 120 python3 tools/diag/idx_ck_debug.py 2>&1 | grep -v amdgpu.ids | head -2
+timeout -k 10 800 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu \
+  tests/test_gpu_bare_decode.py tests/test_gpu_aggregators.py tests/test_gpu_large_p.py > gpurun_out/b24_tests.log 2>&1 || { tail -40 gpurun_out/b24_tests.log; exit 1; }
+tail -1 gpurun_out/b24_tests.log
+for rep in 1 2; do timeout -k 10 200 python3 tools/index_bench.py 2>&1 | grep -v amdgpu.ids || exit 2; done
