@@ -247,8 +247,10 @@ int fc_decode_accumulate(const uint8_t* stream_buf, const int64_t* stream_off,
  *   err         device int32[1]: cleared, then set nonzero on a malformed code (a code
  *               that does not parse, holds more or fewer than P elements, or whose
  *               byte length is not ceil(bits / 8))
- * Each lane parses 4096 bits of a code from a guessed start; the parses
- * resynchronise within a few codes and are stitched. */
+ * Each lane parses a chunk of a code (2048, 4096 or 8192 bits, chosen from nclients
+ * and max_bytes) from a guessed start; the parses resynchronise within a few codes
+ * and are stitched.  The workspace size depends on the same choice:
+ * take it from fc_index_workspace_bytes with the same nclients and max_bytes. */
 int64_t fc_index_workspace_bytes(int32_t nclients, int64_t max_bytes);
 int fc_build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int64_t* nbytes, int32_t nclients,
                    int64_t P, int64_t max_bytes, uint64_t* idx, uint64_t* idxq, int64_t* total_bits, int32_t* err,
