@@ -38,6 +38,24 @@ def test_host_only_entry_points():
   assert lib.fc_encode_workspace_bytes(128, 25_000_000) >= 128 * 24415 * 16
 
 
+def test_index_workspace_follows_the_chunk_choice():
+  """fc_build_index's chunk lanes: the largest of 8192 / 4096 / 2048 bits giving about
+  600 K lanes, min(15, chunk / 256 - 1) checkpoints each; the workspace holds five int64
+  and the checkpoints per lane, plus an int32 per client."""
+  lib = _lib.load()
+
+  def want(n, max_bytes):
+    cb = 8192
+    while cb > 2048 and n * -(-8 * max_bytes // cb) < 600_000:
+      cb //= 2
+    lanes = n * max(1, -(-8 * max_bytes // cb))
+    return (5 + min(15, cb // 256 - 1)) * 8 * lanes + ((4 * n + 255) & ~255)
+
+  for n, mb in [(1024, 12_300_000), (256, 1_400_000), (128, 1_360_000), (2, 100), (1, 0), (300, 15_872)]:
+    assert lib.fc_index_workspace_bytes(n, mb) == want(n, mb), (n, mb)
+  assert lib.fc_index_workspace_bytes(0, 10) == -1
+
+
 def test_argument_validation_without_gpu():
   lib = _lib.load()
   # rejected before any device work: bad sizes / null pointers / bad mode
