@@ -3448,10 +3448,12 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
   uint32_t it = 0;
   bool failed = false;
   int nk = 0;  // (!EMIT, ckp) checkpoints recorded
+  int32_t ckt = ckp ? a.ckb : INT32_MAX;  // the next checkpoint's threshold (past the last: never)
   while (cons < lim) {
-    if (!EMIT && ckp && nk < a.nck && cons >= (nk + 1) * a.ckb) {  // a code start: checkpoint
+    if (!EMIT && cons >= ckt) {  // a code start: checkpoint
       ckp[nk * ckst] = (uint64_t)cons | ((uint64_t)(nsum + (acc4 >> 2)) << 13);
       ++nk;
+      ckt = nk < a.nck ? (nk + 1) * a.ckb : INT32_MAX;
     }
     it = __builtin_amdgcn_readfirstlane(it + 1u);
     if ((it & (kDecBatch - 1)) == 0) r.batch();
