@@ -3279,6 +3279,9 @@ inline int32_t idx_nck(int32_t chunk) { return std::min(15, chunk / 256 - 1); }
 #ifndef FC_IDX_ASYNC
 #define FC_IDX_ASYNC 0
 #endif
+#ifndef FC_IDX_UNIFORM
+#define FC_IDX_UNIFORM 1  // the guessed parse's wave-uniform fast steps (A/B knob)
+#endif
 constexpr uint64_t kCkNone = ~0ull;
 
 struct IdxArgs {
@@ -3461,7 +3464,21 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
     const uint32_t Ls = e >> 26;
     const int32_t dd4 = (int32_t)((e & 0x7Fu) + ((e >> 7) & 0x7Fu));
     const int32_t lend = min(lim, avail);  // a table step's codes must end inside both
-    if (Ls != 0u && cons + (int32_t)Ls <= lend && (!EMIT || acc4 + dd4 < room4)) {
+    bool stepped = false;
+    if (!EMIT && FC_IDX_UNIFORM && __ballot(cons + 2 * kLutBits > lend) == 0) {
+      // the guessed parse with every lane of the wave 24+ bits from its end: two table
+      // steps with no per-lane checks and no divergent branch, as the decoder's (an entry
+      // that takes nothing is all zero; the lane's code is decoded below)
+      r.win <<= Ls;
+      cons += (int32_t)Ls;
+      acc4 += dd4;
+      const uint32_t e2 = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+      const uint32_t L2 = e2 >> 26;
+      r.win <<= L2;
+      cons += (int32_t)L2;
+      acc4 += (int32_t)((e2 & 0x7Fu) + ((e2 >> 7) & 0x7Fu));
+      stepped = Ls != 0u;
+    } else if (Ls != 0u && cons + (int32_t)Ls <= lend && (!EMIT || acc4 + dd4 < room4)) {
       r.win <<= Ls;
       cons += (int32_t)Ls;
       acc4 += dd4;
@@ -3475,7 +3492,9 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
         cons += (int32_t)L2;
         acc4 += d24;
       }
-    } else {
+      stepped = true;
+    }
+    if (!stepped) {
       // one code: from the window's top 32 bits if it fits there (>= 33 valid bits)
       const int64_t p = start + cons;
       if (EMIT) {
