@@ -209,3 +209,17 @@ def test_min_segments_bounds():
     assert codec.auto_segments(1024, P) >= k and codec.auto_segments(2, P) >= k
   with pytest.raises(ValueError):
     codec.min_segments(_lib.MAX_ELEMS + 1)
+
+
+def test_per_stream_workspaces_are_lru_bounded():
+  """codec keeps one encoder workspace per stream, the least recently used dropped past
+  _WS_STREAMS (a side stream's buffer is recorded on that stream, so dropping it is safe)."""
+  from federated_amd import codec  # pylint: disable=g-import-not-at-top
+  bufs = {}
+  for k in range(codec._WS_STREAMS + 3):  # pylint: disable=protected-access
+    assert codec._ws_slot(bufs, ("dev", k), None) is None  # pylint: disable=protected-access
+    bufs[("dev", k)] = k
+  codec._ws_slot(bufs, ("dev", 4), None)  # pylint: disable=protected-access
+  assert len(bufs) <= codec._WS_STREAMS + 1  # pylint: disable=protected-access
+  assert ("dev", 4) in bufs and list(bufs)[-1] == ("dev", 4)  # most recently used last
+  assert ("dev", 0) not in bufs
