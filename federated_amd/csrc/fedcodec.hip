@@ -2658,6 +2658,14 @@ constexpr int kDecStep3Bits16 = FC_DEC_STEP3_BITS;
 #define FC_DEC_LONG_UNROLL 2
 #endif
 constexpr int kDecLongUnroll = FC_DEC_LONG_UNROLL;  // arithmetic decodes per iteration of that loop
+#ifndef FC_DEC_LONG_R1
+#define FC_DEC_LONG_R1 1  // the LONG loop refills once per iteration, not after every code (A/B knob;
+                          // config 2 decode 0.27 -> 0.22 ms, profiles/r04/diag_dec_long_r1.txt)
+#endif
+#ifndef FC_DEC_LONG_R1_CODES
+#define FC_DEC_LONG_R1_CODES 3  // codes per iteration of that loop (2 / 4: config 2 decode 0.25 / 0.23 ms)
+#endif
+constexpr int kDecLongR1Codes = FC_DEC_LONG_R1_CODES;
 constexpr int kDecLongBits = FC_DEC_LONG_BITS;  // segment bits per element for the arithmetic-only loop (0: never)
 // Batch-point loads as inline asm the compiler's wait-count pass does not see:
 // a lane taking its next block would otherwise wait (in-order vmcnt) for the
@@ -3005,8 +3013,16 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     // 8-bit steps): no table steps, one code decoded arithmetically every iteration
     const bool idle = LONG || moved == 0;
     bool stop = false;
+    // R1: one refill per iteration, after its last code. The first code starts with
+    // >= 33 window bits; a later one is taken from the table only when it ends before
+    // the window's last valid bit (the bits past it are zero, so a code that needs
+    // them parses longer than the bits left), arithmetically only with >= 33 bits, and
+    // otherwise waits for the next iteration. Every code leaves >= 1 valid bit, so the
+    // refill restores >= 33.
+    constexpr bool R1 = LONG && GEN && FC_DEC_LONG_R1;
+    constexpr int NU = LONG ? (R1 ? kDecLongR1Codes : kDecLongUnroll) : 1;
 #pragma unroll
-    for (int u = 0; u < (LONG ? kDecLongUnroll : 1); ++u) {  // LONG: codes (each after a refill) per iteration
+    for (int u = 0; u < NU; ++u) {  // LONG: codes per iteration
     if (u > 0 && cons >= total) break;
     bool tdone = false;
     if (GEN && LONG) {
@@ -3016,7 +3032,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       const uint32_t top = (uint32_t)(r.win >> 32);
       const uint32_t e = glut[top >> (32 - kLutBits)];
       const uint32_t L = e & 31u;
-      if (L != 0u) {
+      if (L != 0u && (!R1 || u == 0 || (int32_t)L < fill - cons)) {
         const uint32_t m = __builtin_amdgcn_ubfe(top, 32u - L, e >> 5);
         const int32_t s = __builtin_amdgcn_sbfe((int32_t)e, 10, 1);  // -1: negative
         relb += (e >> 11) << 2;
@@ -3026,8 +3042,9 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
         tdone = true;
       }
     }
-    if (!tdone && idle && (LONG || (it & (kDecLong - 1)) == 0 ||
-                 (FC_DEC_LONG_LANES <= 64 && __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES))) {
+    if (!tdone && idle && (!R1 || u == 0 || fill - cons > 32) &&
+        (LONG || (it & (kDecLong - 1)) == 0 ||
+         (FC_DEC_LONG_LANES <= 64 && __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES))) {
       // right after a refill (>= 33 window bits): one code decoded arithmetically
       const uint32_t top = (uint32_t)(r.win >> 32);
       const uint32_t z1 = (uint32_t)__clz(top);
@@ -3066,7 +3083,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       acc_add_at<PLANE>(relb, v, ptile, hib, err);
       cons += (int32_t)L;
     }
-    if (fill - cons <= 32) {  // (the blocks are zero past the segment end)
+    if ((!R1 || u == NU - 1) && fill - cons <= 32) {  // (the blocks are zero past the segment end)
       const uint32_t w = r.pop32();
       r.win |= (uint64_t)w << (32 - (fill - cons));
       fill += 32;
