@@ -2627,8 +2627,9 @@ __device__ __noinline__ CodeVal slow_code(const uint8_t* base, int64_t cap, uint
 #define FC_DEC_REPL 1  // accumulator copies per workgroup (1, 2 or 4; A/B knob)
 #endif
 #ifndef FC_DEC_QTR_REPL
-#define FC_DEC_QTR_REPL 2  // the same for quarter-tile segments (dense streams: lanes in step on one address;
-                           // config 2 decode 0.32 -> 0.28 ms wall, 4 copies even)
+#define FC_DEC_QTR_REPL 4  // the same for quarter-tile segments (dense streams: lanes in step on one address;
+                           // config 2 decode 0.32 -> 0.28 ms wall at 2 copies, 4 even; after the one-refill
+                           // LONG loop 1 / 2 / 4 copies: 0.244 / 0.220 / 0.212 ms, profiles/r04/diag_dec_qtr_knobs.txt)
 #endif
 #ifndef FC_DEC_BATCH
 #define FC_DEC_BATCH 4

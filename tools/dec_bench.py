@@ -26,9 +26,14 @@ codec.quantize_encode(None, STEP, seeds, _lib.STOCHASTIC, ptrs=ptrs, P=P, out=ba
 out = torch.empty(P, dtype=torch.float32, device=dev)
 print("code bytes %d (%.3f bits per element)" % (int(batch.nbytes().sum()), 8.0 * batch.nbytes().sum() / (C * P)),
       flush=True)
+ts = []
 for it in range(int(os.environ.get("ITERS", 3))):
   torch.cuda.synchronize()
   t0 = time.perf_counter()
   codec.decode_accumulate(batch, want_sum=False, out=out, step=STEP)
   torch.cuda.synchronize()
-  print("decode %d clients: %.2f ms" % (C, (time.perf_counter() - t0) * 1e3))
+  ts.append((time.perf_counter() - t0) * 1e3)
+  print("decode %d clients: %.3f ms" % (C, ts[-1]))
+if len(ts) > 1:  # the last line: the median of the calls after the first
+  rest = sorted(ts[1:])
+  print("decode %d clients: median %.3f ms" % (C, rest[len(rest) // 2]))
