@@ -26,8 +26,14 @@ launch / its launch time vs the 8 TB/s HBM peak):
                     into the encoder, decode, weighted mean (builder.py:77-117)
   config2           128 x 2^20, stochastic step 1/127, sigma 0.25 ("8-bit")
   config3           256 x 4,050,748 (StackOverflow LSTM), stochastic step 1.0
+  bare_decode       the reference's wire path at the headline: the server holds only the
+                    clients' TFC byte strings (elias_gamma_encode.py:97-109) and decodes them
+                    (run_length_gamma_decode, :69-73): fc_build_index rebuilds the decoder
+                    index from the bytes on the device, then decode + dequantise
   config4_share     one GPU's share of config 4 (512 x 11 M over 8 GPUs): 64 x 11 M,
                     stochastic step 0.5 (sigma 1)
+  config4_full      config 4's whole round on one GPU (512 x 11 M): the N = 1
+                    denominator of the driver's 8-GPU config-4 run
   headline_c128     one GPU's share of the 8-GPU headline: 128 x 25 M
   onebit            config 5's codec: 1024 x 25 M one-bit SGD (one_bit_sgd.py:45-112)
   copy              a 16-byte-per-lane HBM copy (the achievable streaming rate)
@@ -67,8 +73,8 @@ from federated_amd import distributed  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 MODES = {"uniform": _lib.UNIFORM, "stochastic": _lib.STOCHASTIC, "dithered": _lib.DITHERED}
-EXTRA = ["headline_uniform", "trainer_round", "config2", "config3", "config4_share", "headline_c128", "onebit",
-         "onebit_c128", "copy"]
+EXTRA = ["headline_uniform", "trainer_round", "bare_decode", "config2", "config3", "config4_share", "config4_full",
+         "headline_c128", "onebit", "onebit_c128", "copy"]
 
 
 def parse():
@@ -409,6 +415,54 @@ def w_onebit(rows, ptrs, P, steps, warmup, stream, name="onebit"):
   }
 
 
+def w_bare_decode(rows, ptrs, P, steps, warmup, stream):
+  """Server decode of bare TFC strings at the headline (stochastic, step 0.5): the
+  headline round's codes are encoded once (untimed); a step is fc_build_index over
+  the streams' bytes alone (the encoder's index is overwritten) + k_decode + the
+  dequantise epilogue.  The result is checked equal to the decode with the
+  encoder's own index."""
+  C = len(rows)
+  dev = rows[0].device
+  step = 0.5
+  seeds = torch.tensor([[1000 + c, 1000 + c] for c in range(C)], dtype=torch.int64, device=dev)
+  batch = sized_batch(P, C, dev, lambda b: codec.quantize_encode(None, step, probe_seeds(seeds), _lib.STOCHASTIC,
+                                                                  ptrs=ptrs, P=P, out=b, stream=stream))
+  codec.quantize_encode(None, step, seeds, _lib.STOCHASTIC, ptrs=ptrs, P=P, out=batch, stream=stream)
+  if len(codec.check_overflow(batch)):
+    raise SystemExit("bare_decode: overflow")
+  batch.join(stream)
+  ref = torch.empty(P, dtype=torch.float32, device=dev)
+  out = torch.empty(P, dtype=torch.float32, device=dev)
+  err = torch.zeros(1, dtype=torch.int32, device=dev)
+  codec.decode_accumulate(batch, want_sum=False, out=ref, step=step, err=err, stream=stream)
+  nb = batch.nbytes()
+  nbytes = torch.from_numpy(nb.astype(np.int64)).to(dev)
+  maxb = int(nb.max())
+  ierr = []
+  tm = Timer(stream)
+  for i in range(warmup + steps):
+    t = tm if i >= warmup else Timer(stream)
+    ierr.append(t.phase("fc_build_index", lambda: codec.index_codes(batch, nbytes, maxb, stream=stream, check=False)))
+    t.phase("k_decode", lambda: codec.decode_accumulate(batch, want_sum=False, out=out, step=step, err=err,
+                                                        stream=stream))
+  ms = tm.ms()
+  if int(err.item()) or any(int(e.item()) for e in ierr) or not bool(torch.equal(out, ref)):
+    raise SystemExit("bare_decode: index rebuild or decode differs from the encoder-index decode")
+  S = float(nb.astype(np.float64).sum())
+  t_step = ms["fc_build_index"] + ms["k_decode"]
+  return {
+      "workload": "bare_decode", "clients": C, "P": P, "mode": "stochastic", "step_size": step,
+      "ms_per_step": round(t_step, 3), "code_GB": round(S / 1e9, 3),
+      "value_GiBps": round(C * P * 4.0 / (t_step * 1e-3) / 2**30, 2),
+      "index_rebuild": {"kernels": "fc_build_index (k_idx_spec/sync/fix/scan/emit/check)",
+                        "launch_ms": round(ms["fc_build_index"], 3),
+                        "code_GBps": round(S / (ms["fc_build_index"] * 1e-3) / 1e9, 1)},
+      "decode": {"kernel": "k_decode", "launch_ms": round(ms["k_decode"], 3),
+                 "alg_GBps": round((S + 4.0 * P) / (ms["k_decode"] * 1e-3) / 1e9, 1)},
+      "note": "value counts the clients' fp32 deltas the decoded round stands for, over the server side only",
+  }
+
+
 def w_copy(dev, stream, steps=10):
   n = 4 << 30
   a = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -439,6 +493,8 @@ def run_extra(name, args, dev, stream, head_rows, head_ptrs):
     return w_onebit(head_rows[:128], head_ptrs[:128], P, max(steps, 10), warmup, stream, name="onebit_c128")
   if name == "copy":
     return w_copy(dev, stream)
+  if name == "bare_decode":
+    return w_bare_decode(head_rows, head_ptrs, P, steps, warmup, stream)
   if name == "headline_c128":  # the first 128 of the headline's client deltas
     return codec_round(name, head_rows[:128], head_ptrs[:128], P, 0.5, _lib.STOCHASTIC, max(steps, 10), warmup,
                        stream)
@@ -447,6 +503,9 @@ def run_extra(name, args, dev, stream, head_rows, head_ptrs):
     step = 1.0 / 127
   elif name == "config4_share":
     rows = make_deltas(64, 11_000_000, 1.0, dev, 11000)
+    step = 0.5
+  elif name == "config4_full":
+    rows = make_deltas(512, 11_000_000, 1.0, dev, 11000)  # the share's 64 deltas are its first 64
     step = 0.5
   else:  # config3
     rows = make_deltas(256, 4_050_748, 1.0, dev, 9000)
@@ -558,8 +617,8 @@ def main():
   g.manual_seed(20251015 + rank)
   npool = args.pool if args.pool > 0 else Cg
   pool = []
-  need_head = not single or args.workload in ("headline_uniform", "trainer_round", "onebit", "headline_c128",
-                                              "onebit_c128")
+  need_head = not single or args.workload in ("headline_uniform", "trainer_round", "bare_decode", "onebit",
+                                              "headline_c128", "onebit_c128")
   for i in range(npool if need_head else 0):
     if npool == Cg:  # a delta per client, seeded by its global index: any --gpus N sums the same round
       g.manual_seed(20251015 + rank * Cg + i)

@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get("FEDCODEC_LIB") or os.path.join(_HERE, "libfedcodec.so
 UNIFORM, STOCHASTIC, DITHERED = 0, 1, 2
 NORM_MEAN_MAGNITUDE, NORM_MAX_MAGNITUDE, NORM_DIMENSIONLESS, NORM_L2, NORM_LINF, NORM_L2_LINF = 1, 2, 3, 4, 5, 6
 TILE_ELEMS = 1024
-MAX_ELEMS = (1 << 28) - 1  # FC_MAX_ELEMS: one client tensor
+MAX_ELEMS = (1 << 30) - (1 << 26)  # FC_MAX_ELEMS: one client tensor
 MAX_ROW_ELEMS = (1 << 26) - 1  # FC_MAX_ROW_ELEMS: one encoder row (longer tensors are segmented)
 
 # (name, restype, argtypes); every symbol declared in include/fedcodec.h.

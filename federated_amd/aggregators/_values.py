@@ -61,7 +61,9 @@ def sharded_rows(value, shape, sharded, multi, group=None):
       rows, vshape, host = to_device_rows(value, torch.float32)
       if vshape != tuple(shape):
         raise ValueError("client value shape %s != %s" % (vshape, tuple(shape)))
-    except ValueError as e:
+    except Exception as e:  # pylint: disable=broad-except
+      # any rejection (ValueError for a shape, TypeError / RuntimeError for a dtype or
+      # device) is flagged through the preamble, so no rank raises alone
       if not multi:
         raise
       bad = e

@@ -155,6 +155,14 @@ def index_codes(batch, nbytes, max_bytes, quarters=None, stream=None, check=True
   quarter index), batch.total_bits.  Returns the device err flag; ``check`` raises
   ValueError (one host sync) when a code is malformed."""
   device = batch.device
+  if stream is not None and stream != torch.cuda.current_stream(device):
+    # run the whole rebuild on `stream`: it first waits for the work queued so far (the
+    # streams' H2D copy, nbytes), and the workspace / err tensors are then allocated on
+    # it, so the caching allocator cannot hand them out while the index kernels run
+    stream.wait_stream(torch.cuda.current_stream(device))
+    nbytes.record_stream(stream)
+    with torch.cuda.stream(stream):
+      return index_codes(batch, nbytes, max_bytes, quarters=quarters, stream=None, check=check)
   C, P = batch.nclients, batch.P
   want_q = quarter_index_wanted(C) if quarters is None else bool(quarters)
   need = int(_lib.load().fc_index_workspace_bytes(C, int(max_bytes)))
@@ -355,12 +363,12 @@ _SEG_WS = SegWorkspace()
 def min_segments(P):
   """Fewest segments that keep every segment one encoder row (<= 2^26 - 1 elements,
   the look-back status's position width): 1 up to that size; longer tensors (up to
-  2^28 - 1, the decoder index's) are always encoded segmented and stitched."""
+  2^30 - 2^26, FC_MAX_ELEMS) are always encoded segmented and stitched."""
   P = int(P)
   if P <= _lib.MAX_ROW_ELEMS:
     return 1
   if P > _lib.MAX_ELEMS:
-    raise ValueError("client tensors hold at most 2^28 - 1 elements (P = %d)" % P)
+    raise ValueError("client tensors hold at most 2^30 - 2^26 elements (P = %d)" % P)
   k = -(-P // (_lib.MAX_ROW_ELEMS - 2 * 2048))
   while P // k // 2048 * 2048 > _lib.MAX_ROW_ELEMS:
     k += 1
@@ -609,6 +617,8 @@ def rlgamma_encode(qs, caps=None):
   if nseg > 1:
     max_cap = int(out.caps_host.max())
     sws = _SEG_WS.get(C, P, nseg, max_cap, device)
+    if sws is None:
+      raise ValueError("cannot segment %d elements into %d segments" % (P, nseg))
     _lib.call("fc_rlgamma_encode_segmented", _lib.ptr(ptrs), C, P, nseg, max_cap, _lib.ptr(out.stream),
               _lib.ptr(out.stream_off), _lib.ptr(out.stream_cap), _lib.ptr(out.idx), _lib.ptr(out.total_bits),
               _lib.ptr(out.overflow), _lib.ptr(sws), sws.numel(), _lib.stream_handle())

@@ -23,7 +23,10 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 
 #include "../../include/fedcodec.h"
 
@@ -241,6 +244,10 @@ constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagPre = 2ull << 62;
 constexpr uint64_t kFlagSlow = 3ull << 62;  // tile left to the exact kernel (terminal)
 constexpr uint64_t kMask36 = (1ull << 36) - 1;
+// Decoder index entries hold (1 + the last nonzero before the unit) modulo 2^28 in
+// bits [63:36] (writers shift a wider value left by 36: the high bits drop).
+constexpr uint32_t kIdxLastMask = (1u << 28) - 1;
+__host__ __device__ __forceinline__ int32_t sext28(uint32_t x) { return ((int32_t)(x << 4)) >> 4; }
 
 __device__ __forceinline__ Seg seg_from_status(uint64_t w1, uint64_t w2, int64_t tile_base) {
   Seg s;
@@ -1121,7 +1128,8 @@ __device__ __forceinline__ void chunk_prepend(ChunkCode& r, int32_t prev) {
 // run code comes from the wave scan); 7 "far" (>= 7: a nonzero here is coded
 // without its run code and flagged, and the caller prepends the exact one).
 // [31:14] code, [13] flag, [12:10] the state for the next pair (already the
-// byte offset of its table region), [4:0] length.
+// byte offset of its table region), [9:8] the pair's nonzero pattern (bit 8: qa,
+// bit 9: qb), [4:0] length (bits 7:5 zero: two entries' lengths add in one op).
 constexpr int kChainStates = 8;
 constexpr uint32_t kChainFar = 7;
 constexpr int kChainLut = kChainStates * 256;
@@ -1154,7 +1162,8 @@ __device__ __forceinline__ uint32_t pair_chain_entry(uint32_t i) {
       run = min(run + 1u, kChainFar);
     }
   }
-  return (code << 14) | (flag << 13) | (run << 10) | len;
+  const uint32_t nzp = (qa != 0 ? 1u : 0u) | (qb != 0 ? 2u : 0u);
+  return (code << 14) | (flag << 13) | (run << 10) | (nzp << 8) | len;
 }
 
 struct ChainCode {
@@ -1172,6 +1181,9 @@ template <int MODE, int DIV, bool PRE, bool MASK = false>
 __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_t g, const uint32_t (&r4)[4],
                                                       float& dist, int32_t& nnz, const uint32_t* clut,
                                                       const uint32_t* plut, uint32_t& sst, int32_t nvalid = 4) {
+  // nnz: the LANE's nonzero count (the caller reduces it over the wave once per
+  // ticket); on the pair-table path the chunk's nonzero mask comes from the table
+  // entries, so no per-element compares are issued there
   uint4 rb = make_uint4(0, 0, 0, 0);
   if (FC_ABL & 8) {
     rb.x = g * 2654435761u; rb.y = rb.x ^ 0x9E3779B9u; rb.z = rb.x + cq.key.k0; rb.w = rb.y ^ cq.key.k1;
@@ -1180,7 +1192,6 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
   }
   const uint32_t rbits[4] = {rb.x, rb.y, rb.z, rb.w};
   float q[4];
-  bool nz[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     float xv = __uint_as_float(r4[k]);
@@ -1200,23 +1211,8 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
     const float dd = DIV == 1 ? sc - rq : xv - rq * cq.step;
     dist = (!MASK || k < nvalid) ? fmaf(dd, dd, dist) : dist;
     q[k] = r;
-    nz[k] = r != 0.0f;
-    nnz += (int32_t)__popcll(__ballot(nz[k]));
   }
   ChainCode r;
-#if FC_NZ_ADDC
-  {
-    const uint64_t b0 = __ballot(nz[0]), b1 = __ballot(nz[1]), b2 = __ballot(nz[2]);
-    uint64_t cj;
-    uint32_t m = nz[3] ? 1u : 0u;
-    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(m), "=s"(cj) : "v"(m), "s"(b2));
-    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(m), "=s"(cj) : "v"(m), "s"(b1));
-    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(m), "=s"(cj) : "v"(m), "s"(b0));
-    r.nzm = m;
-  }
-#else
-  r.nzm = (nz[0] ? 1u : 0u) | (nz[1] ? 2u : 0u) | (nz[2] ? 4u : 0u) | (nz[3] ? 8u : 0u);
-#endif
   const float mabs = vmax3_abs(q[0], q[1], vmax3_abs(q[2], q[3], 0.0f));
   const bool bad = !(mabs < 8192.0f);
   r.acc = 0;
@@ -1232,11 +1228,18 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
     sst = e1 & kChainState;
     const uint32_t l1 = e1 & 31u;
     r.acc = ((uint64_t)(e0 >> 14) << l1) | (e1 >> 14);
-    r.len = (e0 + e1) & 63u;  // bits 9:5 are zero: the two lengths add without interference
+    r.len = (e0 + e1) & 63u;  // bits 7:5 are zero: the two lengths add without interference
     r.pre = (e0 | e1) & kChainFlag;
+    r.nzm = __builtin_amdgcn_ubfe(e0, 8, 2) | (__builtin_amdgcn_ubfe(e1, 8, 2) << 2);
+    nnz += (int32_t)__popc(r.nzm);
     r.lng = 0;  // |q| <= 7: at most 36 bits
     return r;
   } else {
+    bool nz[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nz[k] = q[k] != 0.0f;
+    r.nzm = (nz[0] ? 1u : 0u) | (nz[1] ? 2u : 0u) | (nz[2] ? 4u : 0u) | (nz[3] ? 8u : 0u);
+    nnz += (int32_t)__popc(r.nzm);
     // codes without the chunk's first run code, as quant_code_fast; the caller
     // prepends it when the lane had a nonzero before the chunk
     const uint32_t dv1 = nz[0] ? 1u : 0u;
@@ -1736,7 +1739,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
       //      the lane's very first run code depends on earlier lanes and is
       //      resolved after the scan.
       float dist = 0.0f;
-      int32_t nnz = 0;  // INT_IN: per lane; float input: wave total
+      int32_t nnz = 0;  // INT_IN and CHAIN: per lane; else the wave total
       int32_t lfirst = -1, llast = -1;  // the lane's first / last nonzero (tile-relative)
       uint32_t lng = 0, llen = 0;
       uint64_t cacc[kChunks];
@@ -2105,7 +2108,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     uint32_t ntk = 0;
     uint64_t pw1 = 0, pw2 = 0;  // look-back window (lane i: super-tile t2-64+i); 0: not fetched
     float dist = 0.0f;
-    int32_t nnz = 0;  // INT_IN: per lane; float input: wave total
+    int32_t nnz = 0;  // INT_IN and CHAIN: per lane; else the wave total
     uint32_t lng = 0;  // lane has a long chunk (either tile)
     uint32_t body = 0;
     int32_t sfirst = -1, slast = -1;  // super-tile-relative first / last nonzero
@@ -2301,7 +2304,8 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t2);
     if (fast) {
       const float d = DIV == 1 ? dsum * (cq.step * cq.step) : dsum;  // DIV 1: sums of (sc - r)^2
-      const int32_t n = INT_IN ? wave_sum_i(nnz) : nnz;
+      // per-lane counts (integer input, the chained table) or the wave total
+      const int32_t n = (INT_IN || CHAIN) ? wave_sum_i(nnz) : nnz;
       // one partial per super-tile (its later tiles' slots: 0), one store instruction each
       if (lane < nt) {
         if (a.dist_part) a.dist_part[(int64_t)c * a.T + t0 + lane] = lane == 0 ? d : 0.0f;
@@ -3078,7 +3082,10 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       }
       // the run may come from far before the tile: bound it before scaling to bytes
       const int32_t rel_now = ((int32_t)(relb - my_addr)) >> 2;
-      const uint32_t rel_new = (uint32_t)(rel_now + (int32_t)d);
+      uint32_t rel_new = (uint32_t)(rel_now + (int32_t)d);
+      // a segment's first nonzero after a run of >= 2^27 zeros: the index's previous
+      // nonzero is known modulo 2^28 only (FC_MAX_ELEMS), and so is the sum
+      if (rel_new >= span) rel_new &= kIdxLastMask;
       bad |= rel_new >= span ? 1u : 0u;
       relb = my_addr + 4u * min(rel_new, span - 1);
       acc_add_at<PLANE>(relb, v, ptile, hib, err);
@@ -3213,7 +3220,10 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
         const int64_t soff = a.stream_off[vc], scap = a.stream_cap[vc];
         const uint64_t bstart = e0 & kMask36, bend = e1 & kMask36;
         if (bend <= bstart) continue;
-        const int32_t rel = (int32_t)((int64_t)(e0 >> 36) - 1 - rel_base);  // last nonzero, unit-relative
+        // last nonzero, unit-relative: the index holds 1 + it modulo 2^28, so this is exact
+        // within 2^27 of the unit; a farther one is reached only by a run code longer than
+        // 32 bits, which the slow path reduces modulo 2^28 (decode_segment)
+        const int32_t rel = sext28((uint32_t)((int64_t)(e0 >> 36) - 1 - rel_base));
         int32_t* ptile = PLANE == 2 ? (int32_t*)((int8_t*)a.plane + (int64_t)c * a.plane_stride + unit_base)
                        : PLANE    ? a.plane + (int64_t)c * a.plane_stride + unit_base
                                   : nullptr;
@@ -3592,6 +3602,9 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
   if (failed) return {kIdxFail, nsum};
   if (EMIT) {
     L += acc4 >> 2;
+    // a code whose last element is nonzero and whose last code ends exactly on the
+    // chunk's end leaves the loop with cons == lim before the in-loop end check
+    if (!end->bad && end->bend < 0 && L == a.P - 1 && start + cons == nbits) end->bend = end->total = nbits;
     if (!end->bad && end->bend >= 0) {
       const uint64_t en = ((uint64_t)end->bend & kMask36) | ((uint64_t)(L + 1) << 36);
       for (; u < nu; ++u) idx_put(a, c, u, en);
@@ -3950,18 +3963,28 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // FC_NORM_L2_LINF: one pass for both wrapper norms, norms[c] = ||x||_2 and
 // norms[C + c] = max |x| (builder.py:100-117: clipping and zeroing).
 constexpr int kNormThreads = 1024;
+// Client split (few clients per GPU): client c's tiles are cut into gridDim.x
+// parts, part s = [s ntile / S, (s + 1) ntile / S), one workgroup each, so a
+// GPU's share of 64-128 clients still fills every CU.  Each part writes its
+// float64 sum and max to part[c][s]; k_norms_finalize adds the parts in order
+// (S = 1: the one-workgroup-per-client sums exactly).
+__device__ __forceinline__ void part_range(int64_t ntile, int s, int S, int64_t& lo, int64_t& hi) {
+  lo = ntile * s / S;
+  hi = ntile * (s + 1) / S;
+}
 // ACC: 0 sum |x|, 1 sum x^2, 2 none (max only).  max |x| is always taken.
 template <int ACC, bool PRE>
-__global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* const* xs, int64_t P, int kind,
-                                                               const float* prescale, float* norms) {
+__global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* const* xs, int64_t P,
+                                                               const float* prescale, double* part) {
   __shared__ double red[kNormThreads / 64];
   __shared__ float redm[kNormThreads / 64];
-  const int c = blockIdx.x;
+  const int c = blockIdx.y;
   const float* __restrict__ x = xs[c];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float s0 = PRE ? prescale[2 * c] : 1.0f, s1 = PRE ? prescale[2 * c + 1] : 1.0f;
   const bool aligned = ((uintptr_t)x & 15u) == 0;
-  const int64_t ntile = (P + 2047) / 2048;
+  int64_t tlo, ntile;
+  part_range((P + 2047) / 2048, (int)blockIdx.x, (int)gridDim.x, tlo, ntile);
   // one float64 accumulator per float4 component: independent chains, summed in a
   // fixed order
   double acc4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -3971,7 +3994,7 @@ __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* cons
   typedef const __attribute__((address_space(1))) float* gfptr;
   typedef const __attribute__((address_space(1))) f4v* gf4ptr;
   const gfptr xg = (gfptr)x;
-  for (int64_t tile = wv; tile < ntile; tile += kNormThreads / 64) {
+  for (int64_t tile = tlo + wv; tile < ntile; tile += kNormThreads / 64) {
     const int64_t base = tile * 2048;
     const bool full = base + 2048 <= P && aligned;
     f4v raw[8];
@@ -4022,13 +4045,30 @@ __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* cons
       t += red[w];
       tm = fmaxf(tm, redm[w]);
     }
-    float out = tm;  // FC_NORM_MAX_MAGNITUDE / FC_NORM_LINF
-    if (kind == FC_NORM_MEAN_MAGNITUDE) out = (float)(t / (double)P);
-    if (kind == FC_NORM_DIMENSIONLESS) out = (float)sqrt(t / (double)P);
-    if (kind == FC_NORM_L2 || kind == FC_NORM_L2_LINF) out = (float)sqrt(t);
-    norms[c] = out;
-    if (kind == FC_NORM_L2_LINF) norms[gridDim.x + c] = tm;
+    double* pp = part + 2 * ((int64_t)c * gridDim.x + blockIdx.x);
+    pp[0] = t;
+    pp[1] = (double)tm;
   }
+}
+
+// The norms from the parts of each client, added in part order (one thread per client).
+__global__ void k_norms_finalize(const double* part, int32_t nclients, int32_t nparts, int64_t P, int kind,
+                                 float* norms) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nclients) return;
+  const double* pp = part + 2 * (int64_t)c * nparts;
+  double t = pp[0];
+  float tm = (float)pp[1];
+  for (int s = 1; s < nparts; ++s) {
+    t += pp[2 * s];
+    tm = fmaxf(tm, (float)pp[2 * s + 1]);
+  }
+  float out = tm;  // FC_NORM_MAX_MAGNITUDE / FC_NORM_LINF
+  if (kind == FC_NORM_MEAN_MAGNITUDE) out = (float)(t / (double)P);
+  if (kind == FC_NORM_DIMENSIONLESS) out = (float)sqrt(t / (double)P);
+  if (kind == FC_NORM_L2 || kind == FC_NORM_L2_LINF) out = (float)sqrt(t);
+  norms[c] = out;
+  if (kind == FC_NORM_L2_LINF) norms[nclients + c] = tm;
 }
 
 __global__ __launch_bounds__(kThreads) void k_finalize(const float* dist_part, const int32_t* nnz_part,
@@ -4090,19 +4130,25 @@ __device__ __forceinline__ uint32_t dpp_row_shl(uint32_t x, int n) {
                 : __builtin_amdgcn_update_dpp(0u, x, 0x104, 0xf, 0xf, false);
 }
 
+// Client split as k_client_norms: grid (S, C), part s of client c codes tiles
+// [s ntile / S, (s + 1) ntile / S) (in the client's rotated tile order) and
+// writes its sums to part[c][s] = {S1, S2, A1, A2, count}; k_mask_finalize adds
+// the parts in order and forms the means and the distortion.
+constexpr int kObPart = 5;  // doubles per part
 template <int KIND>
 __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* xs, int64_t P, float thr,
-                                                            int min_distortion, uint32_t* masks,
-                                                            float* means, double* dist) {
+                                                            uint32_t* masks, double* part) {
   __shared__ double red[4][kObWaves];
   __shared__ uint64_t redn[kObWaves];
   __shared__ uint32_t wordbuf[kObWaves][64];
-  const int c = blockIdx.x;
+  const int c = blockIdx.y;
   const float* __restrict__ x = xs[c];
   const int64_t nw = (P + 31) / 32;
   uint32_t* __restrict__ m = masks + (int64_t)c * nw;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t ntile = (P + 2047) / 2048;
+  int64_t tlo, thi;  // this part's tiles, in rotated order
+  part_range(ntile, (int)blockIdx.x, (int)gridDim.x, tlo, thi);
   const bool aligned = ((uintptr_t)x & 15u) == 0;
   // KIND 0: s1 = sum x, s2 = sum x^2, a1 / a2 = the same over x >= thr;
   // KIND 1: s1 = sum |x|, s2 = sum x^2.  Sums of x: float32 partials over a
@@ -4188,13 +4234,13 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
   };
   // software-pipelined: the next tile's loads are in flight while a tile computes
   f4v ra[8], rb[8];
-  if (wv < ntile) load_tile(tile_of(wv), ra);
-  for (int64_t tt = wv; tt < ntile; tt += 2 * kObWaves) {
+  if (tlo + wv < thi) load_tile(tile_of(tlo + wv), ra);
+  for (int64_t tt = tlo + wv; tt < thi; tt += 2 * kObWaves) {
     const int64_t tn = tt + kObWaves;
-    if (tn < ntile) load_tile(tile_of(tn), rb);
+    if (tn < thi) load_tile(tile_of(tn), rb);
     do_tile(tile_of(tt), ra);
-    if (tn >= ntile) break;
-    if (tn + kObWaves < ntile) load_tile(tile_of(tn + kObWaves), ra);
+    if (tn >= thi) break;
+    if (tn + kObWaves < thi) load_tile(tile_of(tn + kObWaves), ra);
     do_tile(tile_of(tn), rb);
   }
   // fixed-order reductions: lanes (shuffle tree), then waves in order
@@ -4220,6 +4266,34 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
       A1 += red[2][w];
       A2 += red[3][w];
       n_ += redn[w];
+    }
+    double* pp = part + kObPart * ((int64_t)c * gridDim.x + blockIdx.x);
+    pp[0] = S1;
+    pp[1] = S2;
+    pp[2] = A1;
+    pp[3] = A2;
+    pp[4] = (double)n_;
+  }
+}
+
+// Means and distortion of each client from its parts, added in part order (one
+// thread per client).
+template <int KIND>
+__global__ void k_mask_finalize(const double* part, int32_t nclients, int32_t nparts, int64_t P,
+                                int min_distortion, float* means, double* dist) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nclients) return;
+  {
+    const double* pp = part + kObPart * (int64_t)c * nparts;
+    double S1 = pp[0], S2 = pp[1], A1 = pp[2], A2 = pp[3];
+    uint64_t n_ = (uint64_t)pp[4];
+    for (int s = 1; s < nparts; ++s) {
+      const double* q = pp + kObPart * s;
+      S1 += q[0];
+      S2 += q[1];
+      A1 += q[2];
+      A2 += q[3];
+      n_ += (uint64_t)q[4];
     }
     float mb, ma;
     double d_;
@@ -4568,18 +4642,32 @@ __global__ __launch_bounds__(256) void k_fwht_pass(float* const* rows, int64_t n
   }
 }
 
-// Measurement utility (bench.py): a plain 16-byte-per-lane grid-stride copy, the
-// achievable HBM streaming rate the codec kernels are compared with.
-__global__ __launch_bounds__(256) void k_copy_f4(uint4* __restrict__ dst, const uint4* __restrict__ src, int64_t n) {
-  // 4 x 16 B per lane in flight: all four loads issue before the stores
-  const int64_t stride = (int64_t)gridDim.x * 1024;
-  int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
-  for (; i + 768 < n; i += stride) {
-    const uint4 a = src[i], b = src[i + 256], c = src[i + 512], d = src[i + 768];
-    dst[i] = a;
-    dst[i + 256] = b;
-    dst[i + 512] = c;
-    dst[i + 768] = d;
+// Measurement utility (bench.py): a 16-byte-per-lane grid-stride copy, the
+// achievable HBM streaming rate the codec kernels are compared with.  Each lane
+// keeps FC_COPY_U 16-B loads in flight (all issued before the stores); FC_COPY_NT
+// makes the loads and stores non-temporal.
+#ifndef FC_COPY_U
+#define FC_COPY_U 4
+#endif
+#ifndef FC_COPY_NT
+#define FC_COPY_NT 0
+#endif
+__global__ __launch_bounds__(256) void k_copy_f4(uint4* __restrict__ dst_, const uint4* __restrict__ src_, int64_t n) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  v4u* __restrict__ dst = (v4u*)dst_;
+  const v4u* __restrict__ src = (const v4u*)src_;
+  constexpr int U = FC_COPY_U;
+  const int64_t stride = (int64_t)gridDim.x * 256 * U;
+  int64_t i = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  for (; i + 256 * (U - 1) < n; i += stride) {
+    v4u v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = FC_COPY_NT ? __builtin_nontemporal_load(src + i + 256 * k) : src[i + 256 * k];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (FC_COPY_NT) __builtin_nontemporal_store(v[k], dst + i + 256 * k);
+      else dst[i + 256 * k] = v[k];
+    }
   }
   for (; i < n; i += 256) dst[i] = src[i];
 }
@@ -4611,29 +4699,34 @@ __global__ void k_floor_keys(const int64_t* seeds, int32_t C, uint4* keys) {
   keys[c] = make_uint4(k.k0, k.k1, k.c2, k.c3);
 }
 
+// Streaming form (round 5): one client per blockIdx.y, its tiles cut into
+// gridDim.x parts (part_range); the client's row pointer and Philox key are
+// loaded once per workgroup (scalar), each wave walks its part's tiles with the
+// next tile's four float4 loads in flight while a tile computes (registers,
+// double-buffered), and nothing but two words per tile is stored.
 template <int MODE>
-__global__ __launch_bounds__(256) void k_quant_floor(const float* const* xs, int32_t C, int64_t P, int32_t T,
-                                                     float rcp, const uint4* keys, float* dist_part,
-                                                     int32_t* nnz_part) {
+__global__ __launch_bounds__(256) void k_quant_floor(const float* const* xs, int64_t P, int32_t T, float rcp,
+                                                     const uint4* keys, float* dist_part, int32_t* nnz_part) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t tickets = (int64_t)C * T;
-  for (int64_t tk = wave; tk < tickets; tk += nw) {
-    const int64_t t = tk / C;
-    const int32_t c = (int32_t)(tk - t * C);
-    const uint4 kk = keys[c];
-    const Key4 key{(uint32_t)__builtin_amdgcn_readfirstlane(kk.x), (uint32_t)__builtin_amdgcn_readfirstlane(kk.y),
-                   (uint32_t)__builtin_amdgcn_readfirstlane(kk.z), (uint32_t)__builtin_amdgcn_readfirstlane(kk.w)};
-    const float* x = xs[c];
-    float4 v[4];
+  const int wv = (int)uniform(threadIdx.x >> 6);
+  const int c = blockIdx.y;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) f4v* gf4ptr;
+  const gf4ptr x = (gf4ptr)xs[c];
+  const uint4 kk = keys[c];
+  const Key4 key{uniform(kk.x), uniform(kk.y), uniform(kk.z), uniform(kk.w)};
+  int64_t tlo, thi;
+  part_range(T, (int)blockIdx.x, (int)gridDim.x, tlo, thi);
+  auto load = [&](int64_t t, f4v (&v)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t e0 = t * kTE + 4 * (64 * j + lane);
-      v[j] = e0 + 3 < P ? *(const float4*)(x + e0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[j] = e0 + 3 < P ? x[e0 >> 2] : f4v{0.f, 0.f, 0.f, 0.f};
     }
+  };
+  auto tile = [&](int64_t t, const f4v (&v)[4]) {
     float dist = 0.0f;
-    int32_t nnz = 0;
+    uint32_t nnz = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t g = (uint32_t)((t * kTE) >> 2) + 64 * j + lane;
@@ -4653,14 +4746,26 @@ __global__ __launch_bounds__(256) void k_quant_floor(const float* const* xs, int
         }
         const float dd = sc - r;
         dist = fmaf(dd, dd, dist);
-        nnz += (int32_t)__popcll(__ballot(r != 0.0f));
+        nnz += (uint32_t)__popcll(__ballot(r != 0.0f));  // scalar unit
       }
     }
     const float d = wave_sum_f(dist);
     if (lane == 0) {
       dist_part[(int64_t)c * T + t] = d;
-      nnz_part[(int64_t)c * T + t] = nnz;
+      nnz_part[(int64_t)c * T + t] = (int32_t)nnz;
     }
+  };
+  f4v va[4], vb[4];
+  const int nw = (int)(blockDim.x >> 6);
+  int64_t t = tlo + wv;
+  if (t < thi) load(t, va);
+  for (; t < thi; t += 2 * nw) {
+    const int64_t tn = t + nw;
+    if (tn < thi) load(tn, vb);
+    tile(t, va);
+    if (tn >= thi) break;
+    if (tn + nw < thi) load(tn + nw, va);
+    tile(tn, vb);
   }
 }
 
@@ -4681,6 +4786,59 @@ int check_launch(const char* what) {
 }
 
 int64_t tiles_for(int64_t P) { return (P + kTE - 1) / kTE; }
+
+// Library-owned device scratch for small per-launch partials (the client-split
+// reductions), one grow-only buffer per (device, stream): calls on one stream run
+// in order, so a stream's buffer is never used by two launches at once.
+void* scratch_for(hipStream_t s, size_t bytes) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> bufs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  std::pair<void*, size_t>& b = bufs[std::make_pair(dev, s)];
+  if (b.second < bytes) {
+    if (b.first) {
+      (void)hipStreamSynchronize(s);  // the old buffer may still be read by this stream's last launch
+      (void)hipFree(b.first);
+      b.first = nullptr;
+      b.second = 0;
+    }
+    const size_t want = std::max<size_t>(bytes, 64 << 10);
+    if (hipMalloc(&b.first, want) != hipSuccess) {
+      b.first = nullptr;
+      return nullptr;
+    }
+    b.second = want;
+  }
+  return b.first;
+}
+
+// Workgroups per client for the per-client streaming passes (k_client_norms,
+// k_mask_encode): about `per_cu` workgroups per CU in all, each part at least 64
+// tiles of 2048 elements.  1024 clients: one each (as before the split).
+int client_parts(int32_t nclients, int64_t ntile, int per_cu) {
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t want = ((int64_t)per_cu * ncu + nclients - 1) / nclients;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, ntile / 64));
+}
+
+template <int KIND>
+int launch_mask_encode(const float* const* xs, int32_t nclients, int64_t P, float thr, int min_distortion,
+                       uint32_t* masks, float* means, double* dist, hipStream_t s) {
+  const int parts = client_parts(nclients, (P + 2047) / 2048, 4);
+  double* part = (double*)scratch_for(s, sizeof(double) * kObPart * (size_t)nclients * parts);
+  if (!part) return fail(-3, "scratch allocation failed");
+  hipLaunchKernelGGL(k_mask_encode<KIND>, dim3((unsigned)parts, (unsigned)nclients), dim3(kObThreads), 0, s, xs, P,
+                     thr, masks, part);
+  if (const int rc = check_launch("k_mask_encode")) return rc;
+  hipLaunchKernelGGL(k_mask_finalize<KIND>, dim3((nclients + 255) / 256), dim3(256), 0, s, (const double*)part,
+                     nclients, parts, P, min_distortion, means, dist);
+  return check_launch("k_mask_finalize");
+}
+
 
 // Workspace: [status n*T*16][header: ticket shards, spin_err, counter2,
 // slow_count][slow_flag n*4] (all zeroed per launch) [slow_list n*4]
@@ -5285,7 +5443,7 @@ int encode_segmented(const float* const* xs, int32_t nclients, int64_t P, float 
                      int64_t workspace_bytes, void* stream, void* stitch_stream = nullptr, bool int_in = false) {
   SegLayout L;
   if (!seg_layout(nclients, P, K, max_cap, L))
-    return fail(-1, "segmented encode: segments must hold 2048 .. 2^26 - 1 elements (P <= 2^28 - 1, K <= 63)");
+    return fail(-1, "segmented encode: segments must hold 2048 .. 2^26 - 1 elements (P <= FC_MAX_ELEMS, K <= 63)");
   if (!xs || !stream_buf || !stream_off || !stream_cap || !idx || !total_bits || !overflow)
     return fail(-1, "null required pointer");
   if (!workspace || workspace_bytes < L.total || ((uintptr_t)workspace & 255))
@@ -5388,7 +5546,7 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
                   const uint64_t* idx, int32_t nclients, int64_t P, int32_t* err, void* stream,
                   int64_t tile_begin = 0, int64_t tile_end = -1, bool reset_err = true) {
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^28 - 1]");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, FC_MAX_ELEMS = 2^30 - 2^26]");
   if (!stream_buf || !stream_off || !stream_cap || !idx || !err) return fail(-1, "null required pointer");
   a.stream_buf = stream_buf;
   a.stream_off = stream_off;
@@ -5472,7 +5630,7 @@ int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int6
                 int64_t P, int64_t max_bytes, uint64_t* idx, uint64_t* idxq, int64_t* total_bits, int32_t* err,
                 void* workspace, int64_t workspace_bytes, void* stream) {
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^28 - 1]");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, FC_MAX_ELEMS = 2^30 - 2^26]");
   if (max_bytes < 0) return fail(-1, "max_bytes must be >= 0");
   if (!stream_buf || !stream_off || !nbytes || !idx || !total_bits || !err) return fail(-1, "null required pointer");
   if (!workspace || workspace_bytes < idx_workspace_bytes(nclients, max_bytes) || ((uintptr_t)workspace & 15))
@@ -5748,7 +5906,7 @@ int fc_decode_accumulate_scaled_bounded(const uint8_t* stream_buf, const int64_t
                                         int32_t qmax, void* workspace, int64_t workspace_bytes, void* stream) {
   if (!out || !client_scale || !workspace) return fail(-1, "null required pointer");
   if (nclients <= 0) return fail(-1, "nclients must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^28 - 1]");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, FC_MAX_ELEMS = 2^30 - 2^26]");
   if ((uintptr_t)workspace & 15u) return fail(-1, "workspace must be 16-byte aligned");
   // |q| <= 127 declared: int8 rows (a quarter of the rows' memset / write / read traffic)
   const bool q8 = qmax > 0 && qmax <= 127;
@@ -5800,7 +5958,7 @@ int fc_vote_lengths(const float* const* xs, int32_t nclients, int64_t P, const f
                     const int64_t* seeds, int mode, int64_t* bits, double* dist, void* workspace,
                     int64_t workspace_bytes, void* stream) {
   if (nclients <= 0 || K <= 0) return fail(-1, "nclients and K must be > 0");
-  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, 2^28 - 1]");
+  if (P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "P must be in [1, FC_MAX_ELEMS = 2^30 - 2^26]");
   if (mode < 0 || mode > 2) return fail(-1, "mode must be 0 (uniform), 1 (stochastic) or 2 (dithered)");
   if (!xs || !steps || !bits || !dist || (mode != FC_UNIFORM && !seeds)) return fail(-1, "null required pointer");
   if (!workspace || workspace_bytes < fc_vote_workspace_bytes(nclients, P, K) || ((uintptr_t)workspace & 15))
@@ -5832,11 +5990,11 @@ int fc_vote_lengths(const float* const* xs, int32_t nclients, int64_t P, const f
 
 int fc_drive_encode(const float* const* xs, int32_t nclients, int64_t P, int min_distortion, uint32_t* masks,
                     float* means, double* dist, void* stream) {
-  if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
+  if (nclients <= 0 || nclients > 65535 || P <= 0) return fail(-1, "bad sizes");
   if (!xs || !masks || !means || !dist) return fail(-1, "null pointer");
-  hipLaunchKernelGGL(k_mask_encode<1>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, 0.0f,
-                     min_distortion, masks, means, dist);
-  if (const int rc = check_launch("k_mask_encode<1>")) return rc;
+  if (const int rc = launch_mask_encode<1>(xs, nclients, P, 0.0f, min_distortion, masks, means, dist,
+                                           (hipStream_t)stream))
+    return rc;
   hipLaunchKernelGGL(k_mask_distortion<1>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, 0.0f,
                      (const float*)means, dist);
   return check_launch("k_mask_distortion<1>");
@@ -5876,7 +6034,7 @@ int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, in
 
 int fc_quantize_floor(const float* const* xs, int32_t nclients, int64_t P, float step, const int64_t* seeds, int mode,
                       float* dist_part, int32_t* nnz_part, void* workspace, int64_t workspace_bytes, void* stream) {
-  if (nclients <= 0 || P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "bad nclients / P");
+  if (nclients <= 0 || nclients > 65535 || P <= 0 || P > FC_MAX_ELEMS) return fail(-1, "bad nclients / P");
   if (mode != FC_UNIFORM && mode != FC_STOCHASTIC) return fail(-1, "floor kernel: uniform or stochastic");
   if (!xs || !seeds || !dist_part || !nnz_part || !workspace || workspace_bytes < 16LL * nclients)
     return fail(-1, "null pointer or workspace below 16 bytes per client");
@@ -5890,14 +6048,15 @@ int fc_quantize_floor(const float* const* xs, int32_t nclients, int64_t P, float
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int32_t T = (int32_t)tiles_for(P);
-  const int64_t waves = std::min<int64_t>((int64_t)nclients * T, (int64_t)ncu * 32);
-  const dim3 grid((unsigned)((waves + 3) / 4));
+  // about 8 workgroups (32 waves) per CU in all; each part >= 64 tiles
+  const int parts = (int)std::max<int64_t>(1, std::min<int64_t>((8LL * ncu + nclients - 1) / nclients, T / 64));
+  const dim3 grid((unsigned)parts, (unsigned)nclients);
   if (mode == FC_UNIFORM)
-    hipLaunchKernelGGL(k_quant_floor<FC_UNIFORM>, grid, dim3(256), 0, s, xs, nclients, P, T, 1.0f / step, keys,
-                       dist_part, nnz_part);
+    hipLaunchKernelGGL(k_quant_floor<FC_UNIFORM>, grid, dim3(256), 0, s, xs, P, T, 1.0f / step, keys, dist_part,
+                       nnz_part);
   else
-    hipLaunchKernelGGL(k_quant_floor<FC_STOCHASTIC>, grid, dim3(256), 0, s, xs, nclients, P, T, 1.0f / step, keys,
-                       dist_part, nnz_part);
+    hipLaunchKernelGGL(k_quant_floor<FC_STOCHASTIC>, grid, dim3(256), 0, s, xs, P, T, 1.0f / step, keys, dist_part,
+                       nnz_part);
   return check_launch("k_quant_floor");
 }
 
@@ -5909,7 +6068,10 @@ int fc_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t n = nbytes / 16;
-  const dim3 grid((unsigned)std::min<int64_t>((n + 1023) / 1024, (int64_t)ncu * 8));
+#ifndef FC_COPY_WG
+#define FC_COPY_WG 8
+#endif
+  const dim3 grid((unsigned)std::min<int64_t>((n + 256 * FC_COPY_U - 1) / (256 * FC_COPY_U), (int64_t)ncu * FC_COPY_WG));
   hipLaunchKernelGGL(k_copy_f4, grid, dim3(256), 0, (hipStream_t)stream, (uint4*)dst, (const uint4*)src, n);
   return check_launch("k_copy_f4");
 }
@@ -5940,15 +6102,22 @@ int fc_client_norms(const float* const* xs, int32_t nclients, int64_t P, int kin
 
 int fc_client_norms_scaled(const float* const* xs, int32_t nclients, int64_t P, int kind, const float* prescale,
                            float* norms, void* stream) {
-  if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
+  if (nclients <= 0 || nclients > 65535 || P <= 0) return fail(-1, "bad sizes");
   if (kind < 1 || kind > 6) return fail(-1, "bad norm kind");
   if (!xs || !norms) return fail(-1, "null pointer");
   const int acc = kind == FC_NORM_MEAN_MAGNITUDE ? 0 : (kind == FC_NORM_MAX_MAGNITUDE || kind == FC_NORM_LINF) ? 2 : 1;
-  void (*kern)(const float* const*, int64_t, int, const float*, float*) =
+  void (*kern)(const float* const*, int64_t, const float*, double*) =
       prescale ? (acc == 0 ? k_client_norms<0, true> : acc == 1 ? k_client_norms<1, true> : k_client_norms<2, true>)
                : (acc == 0 ? k_client_norms<0, false> : acc == 1 ? k_client_norms<1, false> : k_client_norms<2, false>);
-  hipLaunchKernelGGL(kern, dim3(nclients), dim3(kNormThreads), 0, (hipStream_t)stream, xs, P, kind, prescale, norms);
-  return check_launch("k_client_norms");
+  hipStream_t s = (hipStream_t)stream;
+  const int parts = client_parts(nclients, (P + 2047) / 2048, 2);
+  double* part = (double*)scratch_for(s, sizeof(double) * 2 * (size_t)nclients * parts);
+  if (!part) return fail(-3, "scratch allocation failed");
+  hipLaunchKernelGGL(kern, dim3((unsigned)parts, (unsigned)nclients), dim3(kNormThreads), 0, s, xs, P, prescale, part);
+  if (const int rc = check_launch("k_client_norms")) return rc;
+  hipLaunchKernelGGL(k_norms_finalize, dim3((nclients + 255) / 256), dim3(256), 0, s, (const double*)part, nclients,
+                     parts, P, kind, norms);
+  return check_launch("k_norms_finalize");
 }
 
 int fc_finalize(const float* dist_part, const int32_t* nnz_part, int32_t nclients, int64_t P, double* dist,
@@ -5961,11 +6130,10 @@ int fc_finalize(const float* dist_part, const int32_t* nnz_part, int32_t nclient
 
 int fc_onebit_encode(const float* const* xs, int32_t nclients, int64_t P, float threshold, uint32_t* masks,
                      float* means, double* dist, void* stream) {
-  if (nclients <= 0 || P <= 0) return fail(-1, "bad sizes");
+  if (nclients <= 0 || nclients > 65535 || P <= 0) return fail(-1, "bad sizes");
   if (!xs || !masks || !means || !dist) return fail(-1, "null pointer");
-  hipLaunchKernelGGL(k_mask_encode<0>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P, threshold,
-                     0, masks, means, dist);
-  if (const int rc = check_launch("k_mask_encode<0>")) return rc;
+  if (const int rc = launch_mask_encode<0>(xs, nclients, P, threshold, 0, masks, means, dist, (hipStream_t)stream))
+    return rc;
   hipLaunchKernelGGL(k_mask_distortion<0>, dim3(nclients), dim3(kObThreads), 0, (hipStream_t)stream, xs, P,
                      threshold, (const float*)means, dist);
   return check_launch("k_mask_distortion<0>");

@@ -71,8 +71,11 @@ extern "C" {
 #define FC_NORM_L2_LINF 6 /* both wrapper norms in one pass: norms[c] = L2, norms[nclients + c] = LINF */
 
 #define FC_TILE_ELEMS 1024       /* encoder tile (one wavefront) = decoder index granularity */
-#define FC_MAX_ELEMS 268435455LL     /* P limit: 2^28 - 1 elements per client tensor (the decoder
-                                        index holds 1 + the last nonzero in 28 bits) */
+#define FC_MAX_ELEMS 1006632960LL    /* P limit: 2^30 - 2^26 elements per client tensor -- every code
+                                        then fits the decoder index's 36-bit bit offsets (<= 65 bits
+                                        per element).  The index holds 1 + the last nonzero modulo
+                                        2^28: a reader recovers it from the unit it decodes (the
+                                        first code's nonzero lies in that unit) */
 #define FC_MAX_ROW_ELEMS 67108863LL  /* one encoder row (26-bit positions in the look-back status):
                                         fc_quantize_encode(_hinted / _quarters) and fc_rlgamma_encode
                                         take P <= 2^26 - 1; fc_quantize_encode_segmented cuts longer
@@ -322,7 +325,10 @@ int fc_noise_sum(const int64_t* seeds, int32_t nclients, int64_t P, float* noise
                  void* stream);
 
 /* norms[c] = normalize_fn(x_c) (or the wrapper norms) as float32, kind in FC_NORM_*;
- * float64 accumulation in a fixed order. */
+ * float64 accumulation in a fixed order.  nclients <= 65535.  With few clients each
+ * client's row is split over several workgroups (about two per CU in all), whose
+ * float64 partials a second kernel adds in order; the partials live in a small
+ * library-owned device buffer per (device, stream). */
 int fc_client_norms(const float* const* xs, int32_t nclients, int64_t P, int kind,
                     float* norms, void* stream);
 
@@ -341,7 +347,8 @@ int fc_finalize(const float* dist_part, const int32_t* nnz_part, int32_t nclient
 
 /* One-bit SGD (comparison_methods/one_bit_sgd.py): per client the above/below
  * threshold masks (bit-packed, 1 = x >= threshold), the two means and the
- * distortion; decode_sum adds every client's decoded tensor in client order. */
+ * distortion; decode_sum adds every client's decoded tensor in client order.
+ * nclients <= 65535; rows split over workgroups as fc_client_norms (fc_drive_encode too). */
 int fc_onebit_encode(const float* const* xs, int32_t nclients, int64_t P, float threshold,
                      uint32_t* masks, float* means, double* dist, void* stream);
 int fc_onebit_decode_sum(const uint32_t* masks, const float* means, int32_t nclients,

@@ -199,7 +199,7 @@ def test_drive_create_and_builders():
 
 def test_min_segments_bounds():
   """Tensors longer than one encoder row (2^26 - 1) are always segmented, into rows
-  of at most that many elements; beyond the index's 2^28 - 1 elements: ValueError."""
+  of at most that many elements; beyond FC_MAX_ELEMS (2^30 - 2^26): ValueError."""
   from federated_amd import _lib, codec  # pylint: disable=g-import-not-at-top
   assert codec.min_segments(_lib.MAX_ROW_ELEMS) == 1
   for P in (_lib.MAX_ROW_ELEMS + 1, (1 << 26) + 5, 100_000_000, _lib.MAX_ELEMS):

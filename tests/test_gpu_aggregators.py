@@ -488,3 +488,40 @@ def test_mask_encoders_many_tiles(gpu, P):
                    (_lib.NORM_MAX_MAGNITUDE, lambda x: np.abs(x).max())):
     got = codec.client_norms(dev, kind).cpu().numpy()
     np.testing.assert_allclose(got, [fn(x) for x in xs], rtol=1e-6)
+
+
+@pytest.mark.parametrize("C", [1, 16, 64, 128])
+def test_client_split_passes(gpu, C):
+  """Few clients per GPU: k_client_norms and k_mask_encode cut each client's row
+  over several workgroups (fc's client_parts: up to 16 parts here) and add the
+  float64 parts in order.  Masks bit-exact; the L2 / max norms equal the oracle's
+  correctly rounded float32 (oracle.aggregators.l2_norm); means, distortion and
+  DRIVE scales against float64 numpy (one_bit_sgd.py:56-81, drive.py:58-76)."""
+  P = (1 << 21) + 5
+  rng = np.random.default_rng(C)
+  xs = [(rng.standard_normal(P) * (0.5 + (c % 7))).astype(np.float32) for c in range(C)]
+  dev = [torch.from_numpy(x).to(gpu) for x in xs]
+  nw = (P + 31) // 32
+  l2 = codec.client_norms(dev, _lib.NORM_L2).cpu().numpy()
+  mx = codec.client_norms(dev, _lib.NORM_MAX_MAGNITUDE).cpu().numpy()
+  both = codec.client_norms(dev, _lib.NORM_L2_LINF).cpu().numpy()
+  masks, means, dist = codec.onebit_encode(dev, 0.0)
+  masks = masks.cpu().numpy().view(np.uint32).reshape(C, nw)
+  means = means.cpu().numpy().reshape(C, 2)
+  dist = dist.cpu().numpy()
+  _, dmeans, _ = codec.drive_encode(dev)
+  dmeans = dmeans.cpu().numpy().reshape(C, 2)
+  for c in range(0, C, max(1, C // 8)):
+    x = xs[c]
+    assert l2[c] == oagg.l2_norm(x)
+    assert mx[c] == np.abs(x).max() and both[1, c] == mx[c] and both[0, c] == l2[c]
+    ab = x >= 0
+    bits = np.pad(ab.astype(np.uint8), (0, nw * 32 - P)).reshape(nw, 32)
+    np.testing.assert_array_equal(masks[c], np.packbits(bits, axis=1, bitorder="little").view("<u4").reshape(-1))
+    xd = x.astype(np.float64)
+    mb, ma = xd[~ab].sum() / max((~ab).sum(), 1), xd[ab].sum() / max(ab.sum(), 1)
+    np.testing.assert_allclose(means[c], [mb, ma], rtol=1e-6)
+    dec = np.where(ab, means[c, 1], means[c, 0]).astype(np.float32)
+    np.testing.assert_allclose(dist[c], ((x - dec).astype(np.float64) ** 2).sum(), rtol=1e-6)
+    scale = (xd ** 2).sum() / np.abs(xd).sum()
+    np.testing.assert_allclose(dmeans[c], [-scale, scale], rtol=1e-6)

@@ -144,6 +144,11 @@ def _edge_qs():
   out["trailing_across_chunk"] = q
   q = np.concatenate([np.ones(2730, np.int32), np.full(10, 2, np.int32)])  # code start at bit 8190
   out["two_chunks"] = q
+  # last element nonzero and the code ends exactly on a chunk boundary (no trailing run):
+  # 681 * 3 + 5 = 2048, 1362 * 3 + 2 * 5 = 4096, 2729 * 3 + 5 = 8192 bits
+  out["ends_at_2048"] = np.concatenate([np.ones(681, np.int32), np.full(1, 2, np.int32)])
+  out["ends_at_4096"] = np.concatenate([np.ones(1362, np.int32), np.full(2, 2, np.int32)])
+  out["ends_at_8192"] = np.concatenate([np.ones(2729, np.int32), np.full(1, 2, np.int32)])
   return out
 
 

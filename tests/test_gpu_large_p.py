@@ -5,8 +5,9 @@ tensor (builder.py:77-78) and TFC codes any int32 tensor (elias_gamma_encode.py:
 Here a tensor above 2^26 - 1 elements (the encoder's look-back position width) is
 always encoded in segments of at most that many elements -- each continuing its
 client's Philox stream at its element offset -- and stitched into the client's one
-canonical code (codec.min_segments); tensors up to 2^28 - 1 elements (the decoder
-index's width) are accepted.
+canonical code (codec.min_segments); tensors up to FC_MAX_ELEMS = 2^30 - 2^26
+elements are accepted (the decoder index keeps 1 + the last nonzero modulo 2^28,
+recovered from the unit a segment decodes).
 
 Checked through QuantizeEncodeFactory at P = 2^26 + 5 and P = 100,000,000:
 client 0's code byte-identical to the oracle's (the CPU restatement of the TF
@@ -67,6 +68,49 @@ def test_factory_round_beyond_one_encoder_row(gpu, P):
   del rows, batch, out
   torch.cuda.empty_cache()
   # the bare code decoded with an index rebuilt from its bytes
+  s, _ = codec.decode_codes([code0], P)
+  np.testing.assert_array_equal(s.cpu().numpy(), q0)
+  del s
+  torch.cuda.empty_cache()
+
+
+def test_factory_round_beyond_2_28(gpu):
+  """P = 2^28 + 3 (past round 4's 2^28 - 1 cap), uniform rounding, 2 clients; client
+  0 has a zero run of more than 2^27 elements that crosses element 2^28, so the
+  decoder index's last-nonzero field (modulo 2^28) is ambiguous there and the decoder
+  resolves the segment's first nonzero from the unit it decodes.  Client 0's code is
+  byte-identical to the oracle's, the round's result equals the oracle's at sampled
+  positions, and the bare code decodes (index rebuilt from its bytes) to the
+  oracle's q."""
+  P = (1 << 28) + 3
+  C, step = 2, F32(0.5)
+  g = torch.Generator(device=gpu)
+  rows = []
+  for c in range(C):
+    g.manual_seed(777 + c)
+    rows.append(torch.randn(P, generator=g, device=gpu, dtype=torch.float32))
+  z0, z1 = (1 << 27) - 1000, (1 << 28) + 1  # zeros [z0, z1): 2^27 + 1001 elements
+  rows[0][z0:z1] = 0.0
+  process = quantize_encode.QuantizeEncodeFactory(float(step), rounding_type="uniform").create((np.float32, (P,)))
+  out = process.next(process.initialize(), rows)
+  x0 = rows[0].cpu().numpy()
+  q0 = oq.uniform_quantize(x0, step)
+  del x0
+  code0, bits0 = ocodec.run_length_gamma_encode(q0)
+  batch = codec.quantize_encode_checked(rows, float(step), np.zeros((C, 2), np.int64), _lib.UNIFORM)
+  assert batch.client_code(0) == code0
+  del batch
+  idx = np.sort(np.random.default_rng(5).choice(P, 50_000, replace=False))
+  idx = np.concatenate([idx, [0, P - 1, z0 - 1, z0, z1 - 1, z1, (1 << 28) - 1, 1 << 28]]).astype(np.int64)
+  idx = np.unique(idx[idx < P])
+  it = torch.from_numpy(idx).to(gpu)
+  acc = np.zeros(idx.size, np.int64)
+  for c in range(C):
+    acc += oq.uniform_quantize(rows[c][it].cpu().numpy(), step)
+  want = oq.uniform_dequantize(acc.astype(np.int32), step)
+  np.testing.assert_array_equal(out.result[it].cpu().numpy().view(np.uint32), want.view(np.uint32))
+  del rows, out
+  torch.cuda.empty_cache()
   s, _ = codec.decode_codes([code0], P)
   np.testing.assert_array_equal(s.cpu().numpy(), q0)
   del s
