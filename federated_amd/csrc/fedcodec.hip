@@ -136,7 +136,9 @@ __device__ __forceinline__ void philox10_ukey(uint32_t& c0, uint32_t& c1, uint32
     asm volatile("s_add_u32 %0, %1, %2" : "=s"(kk1) : "s"(__builtin_amdgcn_readfirstlane(k1)),
                  "i"(0xBB67AE85u * (uint32_t)r));
     const uint32_t n0 = r < 2 ? (uint32_t)(p1 >> 32) ^ c1 ^ kk0 : xor3_vvs((uint32_t)(p1 >> 32), c1, kk0);
-    const uint32_t n2 = r < 2 ? (uint32_t)(p0 >> 32) ^ c3 ^ kk1 : xor3_vvs((uint32_t)(p0 >> 32), c3, kk1);
+    // (round 2: c3 is still wave-uniform -- the low product of round 1's uniform
+    // c0 -- so c3 ^ kk1 is one scalar xor and n2 one v_xor, no v_mov + v_bitop3)
+    const uint32_t n2 = r < 3 ? (uint32_t)(p0 >> 32) ^ (c3 ^ kk1) : xor3_vvs((uint32_t)(p0 >> 32), c3, kk1);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;
@@ -1177,6 +1179,10 @@ struct ChainCode {
 // quant_code_fast for the chained table: the same quantiser, numerics and
 // counts; sst holds the run state as a byte offset into the chained table
 // (state << 10) and is advanced past the chunk.
+#ifndef FC_PK
+#define FC_PK 0  // packed float32 pairs in quant_code_chain (1): fewer instructions, 2.5 % slower stochastic encode (profiles/r05/diag_enc_pk_ab.txt)
+#endif
+constexpr bool PK = FC_PK;
 template <int MODE, int DIV, bool PRE, bool MASK = false>
 __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_t g, const uint32_t (&r4)[4],
                                                       float& dist, int32_t& nnz, const uint32_t* clut,
@@ -1192,6 +1198,42 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
   }
   const uint32_t rbits[4] = {rb.x, rb.y, rb.z, rb.w};
   float q[4];
+  if (PK && DIV == 1 && !MASK && MODE != FC_DITHERED) {
+    // the same arithmetic with the elementwise multiplies, subtractions and the
+    // distortion terms as packed float32 pairs (v_pk_mul / v_pk_add / v_pk_fma_f32:
+    // one instruction per two elements; IEEE per lane, FTZ as the scalar forms)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 x01 = {__uint_as_float(r4[0]), __uint_as_float(r4[1])};
+    f2 x23 = {__uint_as_float(r4[2]), __uint_as_float(r4[3])};
+    if (PRE) {
+      const f2 s0 = {cq.s0, cq.s0}, s1 = {cq.s1, cq.s1};
+      x01 = (x01 * s0) * s1;
+      x23 = (x23 * s0) * s1;
+    }
+    const f2 rc = {cq.rcp, cq.rcp};
+    const f2 sc01 = x01 * rc, sc23 = x23 * rc;
+    const float sc[4] = {sc01.x, sc01.y, sc23.x, sc23.y};
+    f2 r01, r23;
+    if (MODE == FC_UNIFORM) {
+      r01 = f2{rintf(sc[0]), rintf(sc[1])};
+      r23 = f2{rintf(sc[2]), rintf(sc[3])};
+    } else {
+      const f2 fl01 = {floorf(sc[0]), floorf(sc[1])}, fl23 = {floorf(sc[2]), floorf(sc[3])};
+      const f2 p01 = sc01 - fl01, p23 = sc23 - fl23;
+      const f2 one = {1.0f, 1.0f};
+      const f2 u01v = f2{__uint_as_float((rbits[0] & 0x7FFFFFu) | 0x3F800000u),
+                         __uint_as_float((rbits[1] & 0x7FFFFFu) | 0x3F800000u)} - one;
+      const f2 u23v = f2{__uint_as_float((rbits[2] & 0x7FFFFFu) | 0x3F800000u),
+                         __uint_as_float((rbits[3] & 0x7FFFFFu) | 0x3F800000u)} - one;
+      r01 = f2{u01v.x <= p01.x ? ceilf(sc[0]) : fl01.x, u01v.y <= p01.y ? ceilf(sc[1]) : fl01.y};
+      r23 = f2{u23v.x <= p23.x ? ceilf(sc[2]) : fl23.x, u23v.y <= p23.y ? ceilf(sc[3]) : fl23.y};
+    }
+    const f2 dd01 = sc01 - r01, dd23 = sc23 - r23;
+    f2 dv = dd01 * dd01;
+    dv = __builtin_elementwise_fma(dd23, dd23, dv);
+    dist += dv.x + dv.y;
+    q[0] = r01.x; q[1] = r01.y; q[2] = r23.x; q[3] = r23.y;
+  } else {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     float xv = __uint_as_float(r4[k]);
@@ -1211,6 +1253,7 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
     const float dd = DIV == 1 ? sc - rq : xv - rq * cq.step;
     dist = (!MASK || k < nvalid) ? fmaf(dd, dd, dist) : dist;
     q[k] = r;
+  }
   }
   ChainCode r;
   const float mabs = vmax3_abs(q[0], q[1], vmax3_abs(q[2], q[3], 0.0f));
@@ -4647,10 +4690,10 @@ __global__ __launch_bounds__(256) void k_fwht_pass(float* const* rows, int64_t n
 // keeps FC_COPY_U 16-B loads in flight (all issued before the stores); FC_COPY_NT
 // makes the loads and stores non-temporal.
 #ifndef FC_COPY_U
-#define FC_COPY_U 4
+#define FC_COPY_U 8  // profiles/r05/copy_*.json: 4 / 8 loads in flight, plain / nt: 4.97 / 5.19 / 5.23 / 5.35 TB/s
 #endif
 #ifndef FC_COPY_NT
-#define FC_COPY_NT 0
+#define FC_COPY_NT 1
 #endif
 __global__ __launch_bounds__(256) void k_copy_f4(uint4* __restrict__ dst_, const uint4* __restrict__ src_, int64_t n) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -6051,11 +6094,15 @@ int fc_quantize_floor(const float* const* xs, int32_t nclients, int64_t P, float
   // about 8 workgroups (32 waves) per CU in all; each part >= 64 tiles
   const int parts = (int)std::max<int64_t>(1, std::min<int64_t>((8LL * ncu + nclients - 1) / nclients, T / 64));
   const dim3 grid((unsigned)parts, (unsigned)nclients);
+  // FEDCODEC_FLOOR_LDS (diagnostics): bytes of unused LDS per workgroup, to hold the
+  // floor kernel to the encoder's occupancy (40960: 4 workgroups = 4 waves per SIMD)
+  const char* le = std::getenv("FEDCODEC_FLOOR_LDS");
+  const unsigned lds = le ? (unsigned)std::atoi(le) : 0u;
   if (mode == FC_UNIFORM)
-    hipLaunchKernelGGL(k_quant_floor<FC_UNIFORM>, grid, dim3(256), 0, s, xs, P, T, 1.0f / step, keys, dist_part,
+    hipLaunchKernelGGL(k_quant_floor<FC_UNIFORM>, grid, dim3(256), lds, s, xs, P, T, 1.0f / step, keys, dist_part,
                        nnz_part);
   else
-    hipLaunchKernelGGL(k_quant_floor<FC_STOCHASTIC>, grid, dim3(256), 0, s, xs, P, T, 1.0f / step, keys, dist_part,
+    hipLaunchKernelGGL(k_quant_floor<FC_STOCHASTIC>, grid, dim3(256), lds, s, xs, P, T, 1.0f / step, keys, dist_part,
                        nnz_part);
   return check_launch("k_quant_floor");
 }
