@@ -24,6 +24,7 @@ launch / its launch time vs the 8 TB/s HBM peak):
   trainer_round     the trainer-default builder round at 1024 x 25 M: fused
                     L2 + Linf wrapper-norm pass, clip x weight pre-scale fused
                     into the encoder, decode, weighted mean (builder.py:77-117)
+  trainer_round_c128  the same round on one GPU's 8-GPU share (128 x 25 M)
   config2           128 x 2^20, stochastic step 1/127, sigma 0.25 ("8-bit")
   config3           256 x 4,050,748 (StackOverflow LSTM), stochastic step 1.0
   bare_decode       the reference's wire path at the headline: the server holds only the
@@ -73,8 +74,8 @@ from federated_amd import distributed  # noqa: E402
 
 HBM_PEAK = 8.0e12  # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
 MODES = {"uniform": _lib.UNIFORM, "stochastic": _lib.STOCHASTIC, "dithered": _lib.DITHERED}
-EXTRA = ["headline_uniform", "trainer_round", "bare_decode", "config2", "config3", "config4_share", "config4_full",
-         "headline_c128", "onebit", "onebit_c128", "copy"]
+EXTRA = ["headline_uniform", "trainer_round", "trainer_round_c128", "bare_decode", "config2", "config3",
+         "config4_share", "config4_full", "headline_c128", "onebit", "onebit_c128", "copy"]
 
 
 def parse():
@@ -322,7 +323,7 @@ def codec_round(name, rows, ptrs, P, step, mode, steps, warmup, stream, workload
   }
 
 
-def w_trainer_round(rows, ptrs, P, steps, warmup, stream):
+def w_trainer_round(rows, ptrs, P, steps, warmup, stream, name="trainer_round"):
   """Trainer-default builder round (uniform, step 0.5, clipping + zeroing, weighted),
   device part as builder.WrappedAggregationFactory runs it: ONE fused L2 + Linf norm
   pass, host scalars for the wrapper scales (one 8-KB D2H), the clip scale x weight
@@ -371,17 +372,17 @@ def w_trainer_round(rows, ptrs, P, steps, warmup, stream):
       t_wall.append(time.perf_counter() - w0)
   ms = tm.ms()
   if len(codec.check_overflow(batch)) or int(err.item()):
-    raise SystemExit("trainer_round: overflow or malformed stream")
+    raise SystemExit("%s: overflow or malformed stream" % name)
   S = float(batch.nbytes().astype(np.float64).sum())
   t_round = float(np.mean(t_wall)) * 1e3
   return {
-      "workload": "trainer_round", "clients": C, "P": P, "mode": "uniform", "step_size": step,
+      "workload": name, "clients": C, "P": P, "mode": "uniform", "step_size": step,
       "clipping": True, "zeroing": True, "weighted": True,
       "ms_per_step": round(t_round, 3), "value_GiBps": round(C * P * 4.0 / (t_round * 1e-3) / 2**30, 2),
       "kernels_ms": {k: round(v, 3) for k, v in ms.items()},
       "bits_per_element": round(8 * S / (C * P), 4),
-      "roofline": roofline("k_encode", C * 4.0 * P + S, ms["k_encode"], "trainer_round"),
-      "norms_roofline": roofline("k_client_norms", C * 4.0 * P, ms["k_client_norms"], "trainer_round"),
+      "roofline": roofline("k_encode", C * 4.0 * P + S, ms["k_encode"], name),
+      "norms_roofline": roofline("k_client_norms", C * 4.0 * P, ms["k_client_norms"], name),
   }
 
 
@@ -487,6 +488,9 @@ def run_extra(name, args, dev, stream, head_rows, head_ptrs):
     return codec_round(name, head_rows, head_ptrs, P, 0.5, _lib.UNIFORM, steps, warmup, stream)
   if name == "trainer_round":
     return w_trainer_round(head_rows, head_ptrs, P, steps, warmup, stream)
+  if name == "trainer_round_c128":  # the first 128 of the headline's client deltas
+    return w_trainer_round(head_rows[:128], head_ptrs[:128], P, max(steps, 10), warmup, stream,
+                           name="trainer_round_c128")
   if name == "onebit":
     return w_onebit(head_rows, head_ptrs, P, steps, warmup, stream)
   if name == "onebit_c128":  # config 5's per-GPU share at 8 GPUs: the first 128 client deltas
@@ -617,8 +621,8 @@ def main():
   g.manual_seed(20251015 + rank)
   npool = args.pool if args.pool > 0 else Cg
   pool = []
-  need_head = not single or args.workload in ("headline_uniform", "trainer_round", "bare_decode", "onebit",
-                                              "headline_c128", "onebit_c128")
+  need_head = not single or args.workload in ("headline_uniform", "trainer_round", "trainer_round_c128",
+                                              "bare_decode", "onebit", "headline_c128", "onebit_c128")
   for i in range(npool if need_head else 0):
     if npool == Cg:  # a delta per client, seeded by its global index: any --gpus N sums the same round
       g.manual_seed(20251015 + rank * Cg + i)

@@ -67,6 +67,8 @@ SIGNATURES = {
     "fc_drive_encode": (_INT, [_P, _I32, _I64, _INT, _P, _P, _P, _P]),
     "fc_hadamard": (_INT, [_P, _I32, _I64, _INT, _I64, _I64, _P]),
     "fc_sign_flip": (_INT, [_P, _I32, _I64, _I64, _I64, _P]),
+    "fc_dft_workspace_bytes": (_I64, [_I64]),
+    "fc_dft_rotate": (_INT, [_P, _I32, _I64, _INT, _I64, _I64, _P, _I64, _P]),
     "fc_onebit_decode_sum": (_INT, [_P, _P, _I32, _I64, _P, _P]),
     "fc_onebit_decode_sum_range": (_INT, [_P, _P, _I32, _I64, _I64, _I64, _P, _P]),
 }

@@ -130,8 +130,8 @@ class DiscreteFourierTransformFactory(tc.UnweightedAggregationFactory):
 
   Each client's flattened value is zero-padded to an even length n, sign-flipped by
   the round's Rademacher signs D (``fc_sign_flip``) and rotated by the unitary DFT of
-  its n / 2 complex numbers (first half real, second half imaginary parts; rocFFT via
-  torch.fft); the inner factory aggregates the rotated values; the server applies
+  its n / 2 complex numbers (first half real, second half imaginary parts; the
+  hand-written FFT of fc_dft_rotate); the inner factory aggregates the rotated values; the server applies
   the inverse rotation and drops the padding.  TFF's own pairing of real and
   imaginary parts, sign stream and seed schedule are not available here: parity
   unpinned (round trip, norm preservation and linearity are tested).

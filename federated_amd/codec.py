@@ -858,20 +858,19 @@ def dft_(rows, seed, inverse=False):
   """The DFT rotation of tff.aggregators.DiscreteFourierTransformFactory (builder.py:70-71)
   on device rows of an even length n, in place: forward y = F(D x), with F the unitary
   DFT of the n / 2 complex numbers x[:n/2] + i x[n/2:] returned as (real, imaginary)
-  halves; inverse x = D F^-1(y).  D: ``sign_flip_``; the FFT: torch.fft (rocFFT), a
-  library transform.  F is orthonormal, so the pair round-trips and preserves norms.
+  halves; inverse x = D F^-1(y).  D: the signs of ``sign_flip_``; F: the hand-written
+  FFT of fc_dft_rotate (Stockham radix-16 passes, Bluestein's chirp-z convolution
+  for lengths other than powers of two).  F is orthonormal, so the pair round-trips
+  and preserves norms.
   """
+  _lib.require_gpu()
   n = rows[0].numel()
   if n % 2:
     raise ValueError("the DFT rotation needs an even length (zero-pad first)")
-  h = n // 2
-  if not inverse:
-    sign_flip_(rows, seed)
-  for r in rows:
-    z = torch.complex(r[:h], r[h:])
-    z = torch.fft.fft(z, norm="ortho") if not inverse else torch.fft.ifft(z, norm="ortho")
-    r[:h] = z.real
-    r[h:] = z.imag
-  if inverse:
-    sign_flip_(rows, seed)
+  device = rows[0].device
+  ptrs = _ptr_array(rows, device)
+  need = int(_lib.load().fc_dft_workspace_bytes(n))
+  ws = torch.empty(_round_up(need, 256), dtype=torch.uint8, device=device)
+  _lib.call("fc_dft_rotate", _lib.ptr(ptrs), len(rows), n, int(bool(inverse)), int(seed[0]), int(seed[1]),
+            _lib.ptr(ws), ws.numel(), _lib.stream_handle())
   return rows

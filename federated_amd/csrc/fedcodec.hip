@@ -118,6 +118,9 @@ __device__ __forceinline__ uint32_t xor3_vvs(uint32_t a, uint32_t b, uint32_t s)
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(s));
   return r;
 }
+#ifndef FC_PHILOX_R2S
+#define FC_PHILOX_R2S 1  // round 2's n2 xor with the scalar c3 ^ k1 (A/B knob)
+#endif
 // Rounds 0-1 stay plain C: with a lane-varying c0 only, half of their products
 // and xors are wave-uniform and the compiler moves them to the scalar unit.
 __device__ __forceinline__ void philox10_ukey(uint32_t& c0, uint32_t& c1, uint32_t& c2,
@@ -138,7 +141,7 @@ __device__ __forceinline__ void philox10_ukey(uint32_t& c0, uint32_t& c1, uint32
     const uint32_t n0 = r < 2 ? (uint32_t)(p1 >> 32) ^ c1 ^ kk0 : xor3_vvs((uint32_t)(p1 >> 32), c1, kk0);
     // (round 2: c3 is still wave-uniform -- the low product of round 1's uniform
     // c0 -- so c3 ^ kk1 is one scalar xor and n2 one v_xor, no v_mov + v_bitop3)
-    const uint32_t n2 = r < 3 ? (uint32_t)(p0 >> 32) ^ (c3 ^ kk1) : xor3_vvs((uint32_t)(p0 >> 32), c3, kk1);
+    const uint32_t n2 = r < 2 + FC_PHILOX_R2S ? (uint32_t)(p0 >> 32) ^ (c3 ^ kk1) : xor3_vvs((uint32_t)(p0 >> 32), c3, kk1);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;
@@ -2094,6 +2097,12 @@ constexpr int kEnc2Waves = 4;
 #ifndef FC_LB_LATE
 #define FC_LB_LATE 0  // k_encode2: look-back window loaded after the last tile's codes (A/B knob)
 #endif
+#ifndef FC_FRESH_ARGS
+#define FC_FRESH_ARGS 0  // k_encode2's once-per-ticket fields re-read from the kernel arguments: 0 none,
+                         // 1 partials + index pointers, 2 also the status pointer and T2 (A/B knob:
+                         // fewer SGPR spill reloads, but 1 / 2 took the stochastic encode +1.3 / +2 %,
+                         // the scalar loads' waits: profiles/r05/diag_enc_fresh_ab.txt)
+#endif
 template <int MODE, bool INT_IN, int DIV, bool PRE, int NT>
 __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_encode2(EncodeArgs a) {
   constexpr int STE = NT * kTE;  // elements per super-tile (ticket)
@@ -2344,15 +2353,19 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     const float dsum = INT_IN ? 0.0f : wave_sum_f(dist);
     const bool fast = __ballot(lng != 0) == 0 && kPre + body + 96u <= 32u * kWin2Words &&
                       (INT_IN || dsum <= 3.4028235e38f);
-    uint64_t* st = a.status + 2 * ((int64_t)c * a.T + t2);
+    uint64_t* const status_f = FC_FRESH_ARGS >= 2 ? enc_args_fresh().status : a.status;
+    uint64_t* st = status_f + 2 * ((int64_t)c * a.T + t2);
     if (fast) {
       const float d = DIV == 1 ? dsum * (cq.step * cq.step) : dsum;  // DIV 1: sums of (sc - r)^2
       // per-lane counts (integer input, the chained table) or the wave total
       const int32_t n = (INT_IN || CHAIN) ? wave_sum_i(nnz) : nnz;
       // one partial per super-tile (its later tiles' slots: 0), one store instruction each
       if (lane < nt) {
-        if (a.dist_part) a.dist_part[(int64_t)c * a.T + t0 + lane] = lane == 0 ? d : 0.0f;
-        if (a.nnz_part) a.nnz_part[(int64_t)c * a.T + t0 + lane] = lane == 0 ? n : 0;
+        // (fields used once per ticket re-read from the kernel arguments: fewer SGPRs
+        // held across the loop, fewer spill reloads through VGPR lanes)
+        const EncodeArgs& fa = FC_FRESH_ARGS >= 1 ? enc_args_fresh() : a;
+        if (fa.dist_part) fa.dist_part[(int64_t)c * a.T + t0 + lane] = lane == 0 ? d : 0.0f;
+        if (fa.nnz_part) fa.nnz_part[(int64_t)c * a.T + t0 + lane] = lane == 0 ? n : 0;
       }
     }
     const uint32_t agg_tail = fast ? uniform(win_bits32(win, kPre - 32u + body)) : 0u;
@@ -2379,7 +2392,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           st_agent2(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body, kFlagAgg | agg_tail);
         }
         STAMP(5);
-        excl = lookback_vec<STE>(a.status + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2);
+        excl = lookback_vec<STE>(status_f + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2);
         STAMP(6);
       }
     }
@@ -2394,7 +2407,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       }
       for (int i = lane; i < (int)kWin2Words; i += kEncThreads) win[i] = 0;
     } else {
-      const bool last_st = t2 == a.T2 - 1;
+      const bool last_st = t2 == (FC_FRESH_ARGS >= 2 ? enc_args_fresh().T2 : a.T2) - 1;
       const Seg incl = seg_combine(excl, agg);
       const uint32_t r0 = (uint32_t)(excl.body & 31);
       const uint32_t dfirst = agg.has_nz ? (uint32_t)(agg.first - excl.last) : 0u;
@@ -2419,7 +2432,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           ie = lane == h ? (off & kMask36) | ((uint64_t)(lb + 1) << 36) : ie;
         }
         ie = lane == nt ? (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36) : ie;  // (last_st only)
-        if (lane < nt + (last_st ? 1 : 0)) a.idx[(int64_t)c * (a.T + 1) + t0 + lane] = ie;
+        if (lane < nt + (last_st ? 1 : 0)) (FC_FRESH_ARGS >= 1 ? enc_args_fresh().idx : a.idx)[(int64_t)c * (a.T + 1) + t0 + lane] = ie;
       }
       if (lane == 0) {
         if (t2 > 0)
@@ -4728,6 +4741,156 @@ __global__ __launch_bounds__(256) void k_sign_flip(float* const* rows, int64_t n
     if (4 * g + k < n) x[4 * g + k] *= sign_of(w[k]);
 }
 
+// ---------------------------------------------------------------------------
+// DFT rotation (tff.aggregators.DiscreteFourierTransformFactory, builder.py:70-71):
+// the unitary DFT of the m = n / 2 complex numbers z_k = x[k] + i x[k + m], written
+// back as (real, imaginary) halves.  Power-of-two lengths run a Stockham FFT
+// directly; any other length goes through Bluestein's chirp-z identity
+//   Z_j = c_j sum_k (z_k c_k) conj(c_{j-k}),  c_k = exp(-i pi k^2 / m),
+// a circular convolution of length L = 2^ceil(log2(2m - 1)) done by two forward
+// FFTs and one inverse.  The FFT is a sequence of out-of-place Stockham passes
+// of radix 16 (a last pass of radix 2, 4 or 8): thread j reads the 16 elements
+// j + r N / 16 (coalesced across threads), twiddles them by exp(-+2 pi i k r /
+// (Ns 16)), k = j mod Ns, transforms them in registers and writes them to
+// (j - k) 16 + k + r Ns -- natural order after the last pass, no bit reversal.
+// The chirps reduce k^2 modulo 2m in integer arithmetic before the sine.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// In-register radix-2 DIT DFT of R points (R a power of two <= 16), direction sign
+// (-1 forward, +1 inverse); the twiddles are compile-time constants.
+template <int R>
+__device__ __forceinline__ void dft_reg(float2 (&v)[R], float sign) {
+  constexpr int LG = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : 4;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    int rv = 0;
+#pragma unroll
+    for (int b = 0; b < LG; ++b) rv |= ((i >> b) & 1) << (LG - 1 - b);
+    if (i < rv) {
+      const float2 t = v[i];
+      v[i] = v[rv];
+      v[rv] = t;
+    }
+  }
+  // cos / sin of 2 pi j / 16, j = 0..15
+  constexpr float kc[16] = {1.0f, 0.92387953251128674f, 0.70710678118654752f, 0.38268343236508977f,
+                            0.0f, -0.38268343236508977f, -0.70710678118654752f, -0.92387953251128674f,
+                            -1.0f, -0.92387953251128674f, -0.70710678118654752f, -0.38268343236508977f,
+                            0.0f, 0.38268343236508977f, 0.70710678118654752f, 0.92387953251128674f};
+  constexpr float ks[16] = {0.0f, 0.38268343236508977f, 0.70710678118654752f, 0.92387953251128674f,
+                            1.0f, 0.92387953251128674f, 0.70710678118654752f, 0.38268343236508977f,
+                            0.0f, -0.38268343236508977f, -0.70710678118654752f, -0.92387953251128674f,
+                            -1.0f, -0.92387953251128674f, -0.70710678118654752f, -0.38268343236508977f};
+#pragma unroll
+  for (int len = 2; len <= R; len <<= 1) {
+#pragma unroll
+    for (int i = 0; i < R; i += len) {
+#pragma unroll
+      for (int k = 0; k < len / 2; ++k) {
+        const int t = k * (16 / len);  // exp(sign 2 pi i k / len) = table entry k * 16 / len
+        const float2 w = make_float2(kc[t], sign * ks[t]);
+        const float2 a = v[i + k];
+        const float2 b = k == 0 ? v[i + k + len / 2] : cmul(v[i + k + len / 2], w);
+        v[i + k] = make_float2(a.x + b.x, a.y + b.y);
+        v[i + k + len / 2] = make_float2(a.x - b.x, a.y - b.y);
+      }
+    }
+  }
+}
+
+// One Stockham pass of radix R over N points (N / R threads), sub-transforms of Ns.
+template <int R>
+__global__ __launch_bounds__(256) void k_fft_pass(const float2* __restrict__ src, float2* __restrict__ dst, int64_t N,
+                                                  int64_t Ns, float sign) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t q = N / R;
+  if (j >= q) return;
+  const int64_t k = j & (Ns - 1);
+  float2 v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) v[r] = src[j + r * q];
+  if (Ns > 1) {
+    // exp(sign 2 pi i k / (Ns R)), its powers by complex multiplies
+    float sn, cs;
+    sincospif(2.0f * (float)((double)k / (double)(Ns * R)), &sn, &cs);
+    const float2 w1 = make_float2(cs, sign * sn);
+    float2 w = w1;
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      v[r] = cmul(v[r], w);
+      w = cmul(w, w1);
+    }
+  }
+  dft_reg<R>(v, sign);
+  const int64_t o = (j - k) * R + k;
+#pragma unroll
+  for (int r = 0; r < R; ++r) dst[o + r * Ns] = v[r];
+}
+
+// c_k = exp(-i pi k^2 / m) (conjugated: +i), k^2 reduced modulo 2m exactly.
+__device__ __forceinline__ float2 chirp(int64_t k, int64_t m, bool conj_) {
+  const uint64_t q = (uint64_t)((unsigned __int128)(uint64_t)k * (uint64_t)k % (unsigned __int128)(2 * m));
+  double sn, cs;
+  sincospi((double)q / (double)m, &sn, &cs);
+  return make_float2((float)cs, conj_ ? (float)sn : (float)-sn);
+}
+
+// a_k = z_k (c_k) for k < m (inverse: conj(z_k) first), zero up to L.
+__global__ __launch_bounds__(256) void k_dft_pre(float* const* rows, int32_t c, int64_t m, int64_t L, int bluestein,
+                                                 int conj_in, float2* __restrict__ a) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= L) return;
+  const float* __restrict__ x = rows[c];
+  float2 z = make_float2(0.0f, 0.0f);
+  if (k < m) {
+    z = make_float2(x[k], conj_in ? -x[k + m] : x[k + m]);
+    if (bluestein) z = cmul(z, chirp(k, m, false));
+  }
+  a[k] = z;
+}
+
+// b_l = conj(c_l) on l in (-m, m) arranged circularly over L.
+__global__ __launch_bounds__(256) void k_dft_bvec(int64_t m, int64_t L, float2* __restrict__ b) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= L) return;
+  float2 v = make_float2(0.0f, 0.0f);
+  if (l < m) v = chirp(l, m, true);
+  else if (l > L - m) v = chirp(L - l, m, true);
+  b[l] = v;
+}
+
+__global__ __launch_bounds__(256) void k_cmul(float2* __restrict__ a, const float2* __restrict__ b, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = cmul(a[i], b[i]);
+}
+
+// x[j] = Re(w_j), x[j + m] = Im(w_j), w_j = (c_j) conv_j scale (inverse: conjugated).
+__global__ __launch_bounds__(256) void k_dft_post(const float2* __restrict__ conv, int64_t m, int bluestein,
+                                                  float scale, int conj_out, float* const* rows, int32_t c) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  float* __restrict__ x = rows[c];
+  float2 w = conv[j];
+  if (bluestein) w = cmul(w, chirp(j, m, false));
+  x[j] = w.x * scale;
+  x[j + m] = (conj_out ? -w.y : w.y) * scale;
+}
+
+// k_sign_flip for one row given directly (the DFT rotation's per-row loop).
+__global__ __launch_bounds__(256) void k_sign_flip_row(float* const* rows, int32_t c, int64_t n, Key4 key) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (4 * g >= n) return;
+  float* x = rows[c];
+  const uint4 r = philox_group(key, (uint32_t)g);
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (4 * g + k < n) x[4 * g + k] *= sign_of(w[k]);
+}
+
 // Measurement kernel (not a reference interface; fc_quantize_floor): the encoder's
 // arithmetic floor -- read x, draw TF's Philox4x32-10 stream, the exact quantiser
 // (pow2 step: x * (1 / step); floor, ceil, Uint32ToFloat, compare, select; rintf
@@ -4747,7 +4910,7 @@ __global__ void k_floor_keys(const int64_t* seeds, int32_t C, uint4* keys) {
 // loaded once per workgroup (scalar), each wave walks its part's tiles with the
 // next tile's four float4 loads in flight while a tile computes (registers,
 // double-buffered), and nothing but two words per tile is stored.
-template <int MODE>
+template <int MODE, int DEPTH>
 __global__ __launch_bounds__(256) void k_quant_floor(const float* const* xs, int64_t P, int32_t T, float rcp,
                                                      const uint4* keys, float* dist_part, int32_t* nnz_part) {
   const int lane = threadIdx.x & 63;
@@ -4798,17 +4961,32 @@ __global__ __launch_bounds__(256) void k_quant_floor(const float* const* xs, int
       nnz_part[(int64_t)c * T + t] = (int32_t)nnz;
     }
   };
-  f4v va[4], vb[4];
+  f4v va[4], vb[4], vc[4];
   const int nw = (int)(blockDim.x >> 6);
   int64_t t = tlo + wv;
-  if (t < thi) load(t, va);
-  for (; t < thi; t += 2 * nw) {
-    const int64_t tn = t + nw;
-    if (tn < thi) load(tn, vb);
-    tile(t, va);
-    if (tn >= thi) break;
-    if (tn + nw < thi) load(tn + nw, va);
-    tile(tn, vb);
+  if (DEPTH == 2) {  // the next tile's loads in flight while a tile computes
+    if (t < thi) load(t, va);
+    for (; t < thi; t += 2 * nw) {
+      const int64_t tn = t + nw;
+      if (tn < thi) load(tn, vb);
+      tile(t, va);
+      if (tn >= thi) break;
+      if (tn + nw < thi) load(tn + nw, va);
+      tile(tn, vb);
+    }
+  } else {  // the next two tiles' loads in flight
+    if (t < thi) load(t, va);
+    if (t + nw < thi) load(t + nw, vb);
+    for (; t < thi; t += 3 * nw) {
+      if (t + 2 * nw < thi) load(t + 2 * nw, vc);
+      tile(t, va);
+      if (t + nw >= thi) break;
+      if (t + 3 * nw < thi) load(t + 3 * nw, va);
+      tile(t + nw, vb);
+      if (t + 2 * nw >= thi) break;
+      if (t + 4 * nw < thi) load(t + 4 * nw, vb);
+      tile(t + 2 * nw, vc);
+    }
   }
 }
 
@@ -5726,6 +5904,36 @@ int build_index(const uint8_t* stream_buf, const int64_t* stream_off, const int6
   return check_launch("k_idx_check");
 }
 
+// FFT of N = 2^k points from buf[0] (ping-pong with buf[1]); returns the buffer
+// holding the result.
+int fft_pow2(float2* b0, float2* b1, int64_t N, float sign, hipStream_t s, float2** res) {
+  float2* src = b0;
+  float2* dst = b1;
+  int64_t Ns = 1;
+  while (Ns < N) {
+    const int64_t rem = N / Ns;
+    const int R = rem >= 16 ? 16 : (int)rem;
+    const int64_t q = N / R;
+    const dim3 grid((unsigned)((q + 255) / 256));
+    if (R == 16) hipLaunchKernelGGL(k_fft_pass<16>, grid, dim3(256), 0, s, src, dst, N, Ns, sign);
+    else if (R == 8) hipLaunchKernelGGL(k_fft_pass<8>, grid, dim3(256), 0, s, src, dst, N, Ns, sign);
+    else if (R == 4) hipLaunchKernelGGL(k_fft_pass<4>, grid, dim3(256), 0, s, src, dst, N, Ns, sign);
+    else hipLaunchKernelGGL(k_fft_pass<2>, grid, dim3(256), 0, s, src, dst, N, Ns, sign);
+    if (hipGetLastError() != hipSuccess) return check_launch("k_fft_pass");
+    Ns *= R;
+    std::swap(src, dst);
+  }
+  *res = src;
+  return 0;
+}
+
+int64_t dft_len(int64_t m) {  // FFT length: m itself (power of two) or the Bluestein length
+  if ((m & (m - 1)) == 0) return m;
+  int64_t L = 1;
+  while (L < 2 * m - 1) L <<= 1;
+  return L;
+}
+
 }  // namespace
 
 extern "C" {
@@ -6043,6 +6251,68 @@ int fc_drive_encode(const float* const* xs, int32_t nclients, int64_t P, int min
   return check_launch("k_mask_distortion<1>");
 }
 
+int64_t fc_dft_workspace_bytes(int64_t n) {
+  if (n <= 0 || (n & 1)) return -1;
+  const int64_t m = n / 2;
+  return 3 * dft_len(m) * (int64_t)sizeof(float2);
+}
+
+int fc_dft_rotate(float* const* rows, int32_t nclients, int64_t n, int inverse, int64_t seed0, int64_t seed1,
+                  void* workspace, int64_t workspace_bytes, void* stream) {
+  if (nclients <= 0 || n <= 0 || (n & 1) || n > (1LL << 33)) return fail(-1, "n must be even and positive");
+  if (!rows || !workspace) return fail(-1, "null pointer");
+  if (workspace_bytes < fc_dft_workspace_bytes(n) || ((uintptr_t)workspace & 15))
+    return fail(-1, "DFT workspace too small (fc_dft_workspace_bytes) or misaligned");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t m = n / 2, L = dft_len(m);
+  const bool blue = L != m;
+  float2* w0 = (float2*)workspace;
+  float2* w1 = w0 + L;
+  float2* bb = w1 + L;
+  const dim3 gL((unsigned)((L + 255) / 256)), gm((unsigned)((m + 255) / 256));
+  float2* B = nullptr;
+  if (blue) {  // the chirp filter's spectrum, once per call
+    hipLaunchKernelGGL(k_dft_bvec, gL, dim3(256), 0, s, m, L, w0);
+    if (const int rc = check_launch("k_dft_bvec")) return rc;
+    float2* r = nullptr;
+    if (const int rc = fft_pow2(w0, w1, L, -1.0f, s, &r)) return rc;
+    if (r != bb) {
+      if (hipMemcpyAsync(bb, r, L * sizeof(float2), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return fail(-10, "hipMemcpyAsync");
+    }
+    B = bb;
+  }
+  // one row at a time through the workspace (rows: device array of row pointers)
+  for (int32_t c = 0; c < nclients; ++c) {
+    if (!inverse) {
+      const Key4 key = tf_seed_scramble(seed0, seed1);
+      hipLaunchKernelGGL(k_sign_flip_row, dim3((unsigned)(((n + 3) / 4 + 255) / 256)), dim3(256), 0, s, rows, c, n, key);
+      if (const int rc = check_launch("k_sign_flip_row")) return rc;
+    }
+    hipLaunchKernelGGL(k_dft_pre, gL, dim3(256), 0, s, rows, c, m, L, blue ? 1 : 0, inverse ? 1 : 0, w0);
+    if (const int rc = check_launch("k_dft_pre")) return rc;
+    float2* r = nullptr;
+    if (const int rc = fft_pow2(w0, w1, L, -1.0f, s, &r)) return rc;
+    float scale = (float)(1.0 / std::sqrt((double)m));
+    if (blue) {
+      hipLaunchKernelGGL(k_cmul, gL, dim3(256), 0, s, r, (const float2*)B, L);
+      if (const int rc = check_launch("k_cmul")) return rc;
+      float2* other = r == w0 ? w1 : w0;
+      if (const int rc = fft_pow2(r, other, L, 1.0f, s, &r)) return rc;
+      scale = (float)(1.0 / (std::sqrt((double)m) * (double)L));
+    }
+    hipLaunchKernelGGL(k_dft_post, gm, dim3(256), 0, s, (const float2*)r, m, blue ? 1 : 0, scale, inverse ? 1 : 0, rows,
+                       c);
+    if (const int rc = check_launch("k_dft_post")) return rc;
+    if (inverse) {
+      const Key4 key = tf_seed_scramble(seed0, seed1);
+      hipLaunchKernelGGL(k_sign_flip_row, dim3((unsigned)(((n + 3) / 4 + 255) / 256)), dim3(256), 0, s, rows, c, n, key);
+      if (const int rc = check_launch("k_sign_flip_row")) return rc;
+    }
+  }
+  return 0;
+}
+
 int fc_sign_flip(float* const* rows, int32_t nclients, int64_t n, int64_t seed0, int64_t seed1, void* stream) {
   if (nclients <= 0 || nclients > 65535 || n <= 0 || n > (1LL << 34)) return fail(-1, "bad nclients / n");
   if (!rows) return fail(-1, "null pointer");
@@ -6098,12 +6368,13 @@ int fc_quantize_floor(const float* const* xs, int32_t nclients, int64_t P, float
   // floor kernel to the encoder's occupancy (40960: 4 workgroups = 4 waves per SIMD)
   const char* le = std::getenv("FEDCODEC_FLOOR_LDS");
   const unsigned lds = le ? (unsigned)std::atoi(le) : 0u;
-  if (mode == FC_UNIFORM)
-    hipLaunchKernelGGL(k_quant_floor<FC_UNIFORM>, grid, dim3(256), lds, s, xs, P, T, 1.0f / step, keys, dist_part,
-                       nnz_part);
-  else
-    hipLaunchKernelGGL(k_quant_floor<FC_STOCHASTIC>, grid, dim3(256), lds, s, xs, P, T, 1.0f / step, keys, dist_part,
-                       nnz_part);
+  // FEDCODEC_FLOOR_DEPTH (diagnostics): tiles in flight per wave, 1 (default) or 2
+  const char* de = std::getenv("FEDCODEC_FLOOR_DEPTH");
+  const bool deep = de && std::atoi(de) >= 2;
+  void (*kern)(const float* const*, int64_t, int32_t, float, const uint4*, float*, int32_t*) =
+      mode == FC_UNIFORM ? (deep ? k_quant_floor<FC_UNIFORM, 3> : k_quant_floor<FC_UNIFORM, 2>)
+                         : (deep ? k_quant_floor<FC_STOCHASTIC, 3> : k_quant_floor<FC_STOCHASTIC, 2>);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, xs, P, T, 1.0f / step, keys, dist_part, nnz_part);
   return check_launch("k_quant_floor");
 }
 

@@ -40,6 +40,9 @@
  *                          server sum is fc_onebit_decode_sum with (-scale, +scale)
  *   fc_hadamard            tff.aggregators.HadamardTransformFactory rotation that
  *                          builder.py:68-71 wraps around a codec (randomized FWHT)
+ *   fc_dft_rotate          tff.aggregators.DiscreteFourierTransformFactory rotation
+ *                          (builder.py:70-71): sign flip + unitary DFT (Stockham /
+ *                          Bluestein FFT)
  *   fc_onebit_encode/_decode_sum  OneBitSGDFactory encode/decode_and_sum
  *                          (comparison_methods/one_bit_sgd.py:45-81, 87-112)
  *
@@ -377,6 +380,17 @@ int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, in
  * tff.aggregators.DiscreteFourierTransformFactory, which builder.py:70-71 wraps
  * around a codec (the FFT itself is a library transform, rocFFT). */
 int fc_sign_flip(float* const* rows, int32_t nclients, int64_t n, int64_t seed0, int64_t seed1, void* stream);
+
+/* The DFT rotation of tff.aggregators.DiscreteFourierTransformFactory (builder.py:70-71),
+ * in place on nclients device rows of an even length n (rows: device array of row
+ * pointers), one row at a time: forward x <- F(D x), inverse (inverse = 1) x <- D F^-1(x),
+ * with D = fc_sign_flip's signs and F the unitary DFT of the n / 2 complex numbers
+ * x[k] + i x[k + n/2], written back as (real, imaginary) halves.  Hand-written FFT
+ * (Stockham radix-16 passes; Bluestein's chirp-z convolution for lengths other than
+ * powers of two).  workspace: fc_dft_workspace_bytes(n), 16-byte aligned. */
+int64_t fc_dft_workspace_bytes(int64_t n);
+int fc_dft_rotate(float* const* rows, int32_t nclients, int64_t n, int inverse, int64_t seed0,
+                  int64_t seed1, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Measurement utility (not a reference interface): dst <- src, nbytes a multiple
  * of 16, 16-byte aligned pointers; a grid-stride 16-byte-per-lane copy whose rate

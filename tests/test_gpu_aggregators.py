@@ -391,11 +391,13 @@ def test_hadamard_matches_oracle_and_round_trips(gpu, P):
   np.testing.assert_allclose(t.cpu().numpy()[:P], x, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("P", [1, 2, 3, 1000, 4097, 300_001])
+@pytest.mark.parametrize("P", [1, 2, 3, 32, 1000, 4097, 1 << 17, 300_001, 2_000_006])
 def test_dft_matches_oracle_and_round_trips(gpu, P):
   """The DFT rotation (builder.py:70-71): signs from the same Philox stream as the
-  Hadamard rotation, unitary FFT of the n/2 complex numbers; against a float64
-  numpy restatement, norm-preserving, and inverted back to x."""
+  Hadamard rotation, unitary FFT of the n/2 complex numbers (fc_dft_rotate: Stockham
+  passes for powers of two -- m = 16, 2^16 -- Bluestein otherwise, m = 1,000,003 a
+  prime); against a float64 numpy restatement, norm-preserving, and inverted back
+  to x."""
   rng = np.random.default_rng(P + 1)
   x = rng.standard_normal(P).astype(np.float32)
   n = P + P % 2
@@ -407,6 +409,26 @@ def test_dft_matches_oracle_and_round_trips(gpu, P):
   np.testing.assert_allclose(np.linalg.norm(y.astype(np.float64)), np.linalg.norm(x.astype(np.float64)), rtol=1e-5)
   codec.dft_([t], (7, 9), inverse=True)
   np.testing.assert_allclose(t.cpu().numpy()[:P], x, rtol=1e-4, atol=1e-5)
+
+
+def test_dft_rows_at_25M(gpu):
+  """fc_dft_rotate over two rows of 25,000,000 (m = 12.5 M complex, Bluestein length
+  2^25): each row against numpy's float64 FFT (relative L2 error), and back."""
+  P = 25_000_000
+  rng = np.random.default_rng(25)
+  xs = [rng.standard_normal(P).astype(np.float32) for _ in range(2)]
+  ts = [torch.from_numpy(x).to(gpu) for x in xs]
+  codec.dft_(ts, (3, 4))
+  for x, t in zip(xs, ts):
+    y = t.cpu().numpy().astype(np.float64)
+    want = oagg.dft_forward(x, (3, 4))
+    assert np.linalg.norm(y - want) <= 1e-5 * np.linalg.norm(want)
+  codec.dft_(ts, (3, 4), inverse=True)
+  for x, t in zip(xs, ts):
+    back = t.cpu().numpy().astype(np.float64)
+    assert np.linalg.norm(back - x) <= 1e-5 * np.linalg.norm(x)
+  del ts
+  torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("rotation", ["dft", "hadamard"])
