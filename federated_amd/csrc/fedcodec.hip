@@ -52,7 +52,7 @@ constexpr int kChunks = kTE / (4 * kEncThreads);  // 4 chunks of 4 elements per 
 #define FC_WIN_WORDS 544
 #endif
 constexpr int kWinWords = FC_WIN_WORDS;  // per-wave LDS bit window (17 Kbit, ~16.9 bits/element)
-constexpr uint32_t kNoPos = 0x1FFF; // "no nonzero" in a 13-bit tile-relative field
+constexpr uint32_t kNoPos = 0x3FFF; // "no nonzero" in a 14-bit (super-)tile-relative field
 // Ticket streams: one device-scope atomic word saturates near 90 dequeues/us
 // (MI355X_MICROARCH.md "dequeue"), so tickets come from kTicketShards counters,
 // one 64-B line each; stream k hands out tickets k, k + K, k + 2K, ... in order.
@@ -242,13 +242,17 @@ __device__ __forceinline__ Seg seg_combine(const Seg& a, const Seg& b) {
 
 // Status words (two self-tagged 8-byte granules per tile, agent-scope atomics):
 //  w1: [63:62] flag (1 aggregate, 2 inclusive prefix)
-//      aggregate: [61:49] first_rel  [48:36] last_rel  [35:0] body bits
+//      aggregate: [61:48] first_rel  [47:34] last_rel  [33:0] body bits (< 2^32)
 //      prefix:    [61:36] last+1     [35:0] bits
 //  w2: [63:62] flag  [31:0] tail
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagPre = 2ull << 62;
 constexpr uint64_t kFlagSlow = 3ull << 62;  // tile left to the exact kernel (terminal)
 constexpr uint64_t kMask36 = (1ull << 36) - 1;
+constexpr int kAggFirstShift = 48, kAggLastShift = 34;  // aggregate position fields
+__device__ __forceinline__ uint64_t agg_word(uint64_t fr, uint64_t lr, uint32_t body) {
+  return kFlagAgg | (fr << kAggFirstShift) | (lr << kAggLastShift) | (uint64_t)body;
+}
 // Decoder index entries hold (1 + the last nonzero before the unit) modulo 2^28 in
 // bits [63:36] (writers shift a wider value left by 36: the high bits drop).
 constexpr uint32_t kIdxLastMask = (1u << 28) - 1;
@@ -262,12 +266,12 @@ __device__ __forceinline__ Seg seg_from_status(uint64_t w1, uint64_t w2, int64_t
     s.last = (int32_t)((w1 >> 36) & ((1u << 26) - 1)) - 1;
     s.body = w1 & kMask36;
   } else {
-    const uint32_t fr = (uint32_t)(w1 >> 49) & 0x1FFF;
-    const uint32_t lr = (uint32_t)(w1 >> 36) & 0x1FFF;
+    const uint32_t fr = (uint32_t)(w1 >> kAggFirstShift) & kNoPos;
+    const uint32_t lr = (uint32_t)(w1 >> kAggLastShift) & kNoPos;
     s.has_nz = fr != kNoPos;
     s.first = (int32_t)(tile_base + fr);
     s.last = (int32_t)(tile_base + lr);
-    s.body = w1 & kMask36;
+    s.body = w1 & ((1ull << kAggLastShift) - 1);
   }
   s.tail = (uint32_t)w2;
   return s;
@@ -598,9 +602,9 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
       r.tail = __builtin_amdgcn_readlane(l2, 63);
       return seg_combine(r, S);
     }
-    // aggregates above the prefix: [61:49] first_rel, [48:36] last_rel, body < 2^32
+    // aggregates above the prefix: [61:48] first_rel, [47:34] last_rel, body < 2^32
     const bool agg = lane > p;
-    const uint32_t fr = (h1 >> 17) & 0x1FFFu, lr = (h1 >> 4) & 0x1FFFu;
+    const uint32_t fr = (h1 >> (kAggFirstShift - 32)) & kNoPos, lr = (h1 >> (kAggLastShift - 32)) & kNoPos;
     const bool nz = agg && fr != kNoPos;
     const int32_t tb = ti * SPAN;
     int32_t lastv = agg ? -1 : (lane == p ? plast : -1);
@@ -740,9 +744,9 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     r.tail = __builtin_amdgcn_readlane(l2, 63);
     return r;
   }
-  // aggregates above the prefix: [61:49] first_rel, [48:36] last_rel, body < 2^32
+  // aggregates above the prefix: [61:48] first_rel, [47:34] last_rel, body < 2^32
   const bool agg = lane > p;
-  const uint32_t fr = (h1 >> 17) & 0x1FFFu, lr = (h1 >> 4) & 0x1FFFu;
+  const uint32_t fr = (h1 >> (kAggFirstShift - 32)) & kNoPos, lr = (h1 >> (kAggLastShift - 32)) & kNoPos;
   const bool nz = agg && fr != kNoPos;
   const int32_t tb = ti * SPAN;
   int32_t lastv = agg ? -1 : (lane == p ? plast : -1);
@@ -1913,7 +1917,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
           } else {
             const uint64_t fr = tile_last >= 0 ? (uint64_t)tile_first : kNoPos;
             const uint64_t lr = tile_last >= 0 ? (uint64_t)tile_last : kNoPos;
-            st_agent2(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body, kFlagAgg | agg_tail);
+            st_agent2(st, agg_word(fr, lr, body), kFlagAgg | agg_tail);
           }
         }
         nv = true;
@@ -2059,15 +2063,22 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
 #ifndef FC_PAIR_CHAIN
 #define FC_PAIR_CHAIN 1  // k_encode2: the chained pair table (run state across the lane's chunks)
 #endif
+#ifndef FC_ENC2_WAVES
+#define FC_ENC2_WAVES 8  // k_encode2 waves per workgroup (4 or 8; two 8-wave workgroups per CU)
+#endif
 #ifndef FC_WIN2_WORDS
-// the chained table's 8 KiB come out of the windows: four 4-wave workgroups per CU
-#define FC_WIN2_WORDS (FC_PAIR_CHAIN ? 952 : 2 * FC_WIN_WORDS)
+// LDS per CU (160 KiB) = workgroups x (tables + waves x (window + 4 KiB staging)):
+// the chained table's 9 KiB shared by eight waves leave 1240-word windows (two
+// 8-wave workgroups per CU), by four 952 (four 4-wave workgroups)
+#define FC_WIN2_WORDS (FC_PAIR_CHAIN ? (FC_ENC2_WAVES == 8 ? 1240 : 952) : 2 * FC_WIN_WORDS)
 #endif
 constexpr uint32_t kWin2Words = FC_WIN2_WORDS;
-// four-tile tickets while codes are expected within this many bits per element
-// (their window holds 32 * kWin2Words - kPre - 96 bits = ~7.4 bits per element with
-// the chained pair table, ~8.4 without)
-constexpr double kNt4Bits = 6.5;
+// NT-tile tickets while codes are expected within this many bits per element: a
+// window holds 32 * kWin2Words - kPre - 96 bits (1240 words: ~9.6 bits per element
+// for four tiles, ~4.8 for eight); the host's expectation is the caller's
+// capacity hint (the last round's largest code + 1/8)
+constexpr double kNt4Bits = FC_ENC2_WAVES == 8 ? 8.5 : 6.5;
+constexpr double kNt8Bits = FC_ENC2_WAVES == 8 ? 4.4 : 0.0;
 constexpr int kSTE = 2 * kTE;  // elements per super-tile
 
 // LDS-DMA of one full, 16-B-aligned tile into the staging (as stage_tile).
@@ -2090,7 +2101,7 @@ __device__ __forceinline__ bool stage_at(const uint32_t* x, int64_t tile_base, i
 // Four independent waves per workgroup: they share the code tables (LDS per wave
 // = window + staging + a quarter of the tables), nothing else -- each takes its
 // own tickets; the only barrier is after the tables are built.
-constexpr int kEnc2Waves = 4;
+constexpr int kEnc2Waves = FC_ENC2_WAVES;
 #ifndef FC_PAIR_LUT
 #define FC_PAIR_LUT 1
 #endif
@@ -2164,8 +2175,8 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     uint32_t lng = 0;  // lane has a long chunk (either tile)
     uint32_t body = 0;
     int32_t sfirst = -1, slast = -1;  // super-tile-relative first / last nonzero
-    uint32_t bodyb[NT];   // body bits before tile h
-    int32_t lastb[NT];    // last nonzero before tile h (super-tile-relative, -1 none)
+    uint32_t bodyv = 0;   // lane h: body bits before tile h
+    int32_t lastv = -1;   // lane h: last nonzero before tile h (super-tile-relative, -1 none)
     for (int h = 0; h < NT; ++h) {
       if (h >= 1) {
         if (h >= nt) break;
@@ -2340,8 +2351,8 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         const uint64_t fm = __ballot(lfirst >= 0);  // lanes are in element order
         sfirst = fm ? __builtin_amdgcn_readlane(lfirst, (int)__builtin_ctzll(fm)) : -1;
       }
-      bodyb[h] = body;
-      lastb[h] = slast;
+      bodyv = lane == h ? body : bodyv;
+      lastv = lane == h ? slast : lastv;
       slast = hlast >= 0 ? hlast : slast;
       body += hbody;
     }
@@ -2389,7 +2400,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         if (lane == 0) {
           const uint64_t fr = slast >= 0 ? (uint64_t)sfirst : kNoPos;
           const uint64_t lr = slast >= 0 ? (uint64_t)slast : kNoPos;
-          st_agent2(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body, kFlagAgg | agg_tail);
+          st_agent2(st, agg_word(fr, lr, body), kFlagAgg | agg_tail);
         }
         STAMP(5);
         excl = lookback_vec<STE>(status_f + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2);
@@ -2424,13 +2435,11 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         }
       }
       {  // decoder index entries of the super-tile's tiles (+ the row's end entry), lane h: tile t0 + h
-        uint64_t ie = (excl.body & kMask36) | ((uint64_t)(excl.last + 1) << 36);
-#pragma unroll
-        for (int h = 1; h < NT; ++h) {  // later tiles: after the earlier tiles' codes (and the run code before them)
-          const uint64_t off = excl.body + (lastb[h] >= 0 ? (uint64_t)R0 + bodyb[h] : 0u);
-          const int32_t lb = lastb[h] >= 0 ? (int32_t)(sbase + lastb[h]) : excl.last;
-          ie = lane == h ? (off & kMask36) | ((uint64_t)(lb + 1) << 36) : ie;
-        }
+        // tile h: after the earlier tiles' codes (and the run code before them); tile 0
+        // (lastv -1): the exclusive prefix itself
+        const uint64_t off = excl.body + (lastv >= 0 ? (uint64_t)R0 + bodyv : 0u);
+        const int32_t lb = lastv >= 0 ? (int32_t)(sbase + lastv) : excl.last;
+        uint64_t ie = (off & kMask36) | ((uint64_t)(lb + 1) << 36);
         ie = lane == nt ? (incl.body & kMask36) | ((uint64_t)(incl.last + 1) << 36) : ie;  // (last_st only)
         if (lane < nt + (last_st ? 1 : 0)) (FC_FRESH_ARGS >= 1 ? enc_args_fresh().idx : a.idx)[(int64_t)c * (a.T + 1) + t0 + lane] = ie;
       }
@@ -2548,7 +2557,7 @@ __global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
       if (lane == 0) {
         const uint64_t fr = agg.has_nz ? (uint64_t)tile_first : kNoPos;
         const uint64_t lr = agg.has_nz ? (uint64_t)tile_last : kNoPos;
-        st_agent2(st, kFlagAgg | (fr << 49) | (lr << 36) | (uint64_t)body, kFlagAgg | agg.tail);
+        st_agent2(st, agg_word(fr, lr, (uint32_t)body), kFlagAgg | agg.tail);
       }
       bool slow = false;
       excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, slow);
@@ -5173,11 +5182,12 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   void (*kern)(EncodeArgs) = nullptr;
   void (*kern2)(EncodeArgs) = nullptr;
   void (*kern4)(EncodeArgs) = nullptr;
+  void (*kern8)(EncodeArgs) = nullptr;
   void (*exact)(EncodeArgs) = nullptr;
   const bool pre = !int_in && prescale != nullptr;
 #define FC_PICK(M, I, D, Q)                                                                       \
   (kern = k_encode<M, I, D, Q>, kern2 = k_encode2<M, I, D, Q, 2>, kern4 = k_encode2<M, I, D, Q, 4>, \
-   exact = k_encode_exact<M, I, D == 1>)
+   kern8 = k_encode2<M, I, D, Q, 8>, exact = k_encode_exact<M, I, D == 1>)
 #define FC_PICK2(M, D) (pre ? FC_PICK(M, false, D, true) : FC_PICK(M, false, D, false))
 #define FC_PICK3(M) (pow2 ? FC_PICK2(M, 1) : mark ? FC_PICK2(M, 2) : FC_PICK2(M, 0))
   if (int_in) FC_PICK(FC_UNIFORM, true, 0, false);
@@ -5209,17 +5219,19 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   // by the caller's largest stream capacity (host-known): codes expected within
   // kNt4Bits bits per element (+ slack) take four-tile tickets; denser ones, or an
   // unknown capacity, two (a window overflow sends the client to the exact path)
-  int nt = (max_cap > 0 && 8.0 * (double)max_cap <= kNt4Bits * (double)P + 8.0 * 8192.0) ? 4 : 2;
-  if (const char* e = getenv("FEDCODEC_ENC_NT")) nt = atoi(e) == 4 ? 4 : 2;  // test knob
+  // (eight-tile tickets, FC_ENC2_WAVES 8: 1024 x 25 M stochastic 29.7 -> see DESIGN §5)
+  const double hint_bits = max_cap > 0 ? (8.0 * (double)max_cap - 8.0 * 8192.0) / (double)P : 1e9;
+  int nt = hint_bits <= kNt8Bits ? 8 : hint_bits <= kNt4Bits ? 4 : 2;
+  if (const char* e = getenv("FEDCODEC_ENC_NT")) nt = atoi(e) == 8 && kNt8Bits > 0 ? 8 : atoi(e) == 4 ? 4 : 2;  // test knob
   // with four-tile tickets (and the chained pair table) from 512 clients on a full
   // chip: 512 x 25 M stochastic 22.1 (k_encode) -> 15.9 ms, uniform 19.6 -> 15.3
   // (profiles/r03/diag_enc512.txt); fewer clients are segmented (codec.auto_segments)
-  const int64_t rows_per_wave = nt == 4 ? 8 : 4;
+  const int64_t rows_per_wave = nt >= 4 ? 8 : 4;
   bool super = (int64_t)ncu * per_cu0 * kEnc2Waves <= rows_per_wave * nclients && T >= 2;
   if (const char* e = getenv("FEDCODEC_ENC2")) super = atoi(e) != 0;  // test knob
   if (idxq) super = false;  // quarter-tile entries come from the one-tile kernel (few clients)
   if (super) {
-    kern = nt == 4 ? kern4 : kern2;
+    kern = nt == 8 ? kern8 : nt == 4 ? kern4 : kern2;
     a.T2 = (int32_t)((T + nt - 1) / nt);
   }
   const int wpg = super ? kEnc2Waves : 1;  // waves per workgroup

@@ -27,7 +27,7 @@ from test_gpu_codec import MODES, ORACLE_Q
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["2", "4"], ids=["2tiles", "4tiles"])
+@pytest.fixture(autouse=True, params=["2", "4", "8"], ids=["2tiles", "4tiles", "8tiles"])
 def _super_tiles(monkeypatch, request):
   monkeypatch.setenv("FEDCODEC_ENC2", "1")
   monkeypatch.setenv("FEDCODEC_ENC_NT", request.param)

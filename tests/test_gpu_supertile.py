@@ -6,8 +6,8 @@ run k_encode.  FEDCODEC_ENC2=1 forces the super-tile kernel for every launch, so
 the same oracle checks cover it: integer input (run-length gamma of int32),
 the three roundings with partial, odd-count and single tiles, the division
 variants, per-client norms (QSGD), the TFF pre-scale (trainer round), the
-multi-window look-back, and the reference's known answers -- with two and
-with four tiles per ticket.
+multi-window look-back, and the reference's known answers -- with two, four
+and eight tiles per ticket.
 """
 import pytest
 
@@ -22,9 +22,10 @@ from test_gpu_configs import test_config1_trainer_defaults_round, test_config_ro
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["2", "4"], ids=["2tiles", "4tiles"])
+@pytest.fixture(autouse=True, params=["2", "4", "8"], ids=["2tiles", "4tiles", "8tiles"])
 def _super_tiles(monkeypatch, request):
-  """Both ticket sizes: two tiles, and four (FEDCODEC_ENC_NT=4: the per-ticket work
-  once per 4096 elements, a window of ~8.4 bits per element before the exact path)."""
+  """The three ticket sizes: two tiles, four and eight (FEDCODEC_ENC_NT=8: the
+  per-ticket work once per 8192 elements, a window of ~4.8 bits per element before
+  the exact path, so the denser cases here also take the exact re-encode)."""
   monkeypatch.setenv("FEDCODEC_ENC2", "1")
   monkeypatch.setenv("FEDCODEC_ENC_NT", request.param)
