@@ -1194,9 +1194,9 @@ template <int MODE, int DIV, bool PRE, bool MASK = false>
 __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_t g, const uint32_t (&r4)[4],
                                                       float& dist, int32_t& nnz, const uint32_t* clut,
                                                       const uint32_t* plut, uint32_t& sst, int32_t nvalid = 4) {
-  // nnz: the LANE's nonzero count (the caller reduces it over the wave once per
-  // ticket); on the pair-table path the chunk's nonzero mask comes from the table
-  // entries, so no per-element compares are issued there
+  // r.nzm: the chunk's nonzero mask (the caller counts the lane's nonzeros from the
+  // masks once per tile); on the pair-table path it comes from the table entries, so
+  // no per-element compares are issued there
   uint4 rb = make_uint4(0, 0, 0, 0);
   if (FC_ABL & 8) {
     rb.x = g * 2654435761u; rb.y = rb.x ^ 0x9E3779B9u; rb.z = rb.x + cq.key.k0; rb.w = rb.y ^ cq.key.k1;
@@ -1281,7 +1281,6 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
     r.len = (e0 + e1) & 63u;  // bits 7:5 are zero: the two lengths add without interference
     r.pre = (e0 | e1) & kChainFlag;
     r.nzm = __builtin_amdgcn_ubfe(e0, 8, 2) | (__builtin_amdgcn_ubfe(e1, 8, 2) << 2);
-    nnz += (int32_t)__popc(r.nzm);
     r.lng = 0;  // |q| <= 7: at most 36 bits
     return r;
   } else {
@@ -1289,7 +1288,6 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
 #pragma unroll
     for (int k = 0; k < 4; ++k) nz[k] = q[k] != 0.0f;
     r.nzm = (nz[0] ? 1u : 0u) | (nz[1] ? 2u : 0u) | (nz[2] ? 4u : 0u) | (nz[3] ? 8u : 0u);
-    nnz += (int32_t)__popc(r.nzm);
     // codes without the chunk's first run code, as quant_code_fast; the caller
     // prepends it when the lane had a nonzero before the chunk
     const uint32_t dv1 = nz[0] ? 1u : 0u;
@@ -1445,6 +1443,20 @@ constexpr uint32_t kPre = 96;
 #ifndef FC_EMIT_BRANCH
 #define FC_EMIT_BRANCH 1  // empty codes skip their ORs by a branch (0: their zero ORs go to lane-spread words)
 #endif
+// The window ORs as inline asm (FC_EMIT_ASM): the compiler's wait-count pass
+// otherwise puts an s_waitcnt vmcnt(0) in front of the first OR of a tile -- it
+// cannot tell the window from the staging buffer the next tile's LDS-DMA is
+// filling -- so the emission waited for that DMA (and every pending store).  LDS
+// operations of one wave complete in order, so the later window reads see the ORs.
+#ifndef FC_EMIT_ASM
+#define FC_EMIT_ASM 0  // measured even (profiles/r05/diag_enc_nt_ab.txt, easm)
+#endif
+typedef __attribute__((address_space(3))) uint32_t* lds_uptr;
+template <int OFS>
+__device__ __forceinline__ void lds_or(uint32_t* p, uint32_t v) {
+  if (FC_EMIT_ASM) asm volatile("ds_or_b32 %0, %1 offset:%2" ::"v"((lds_uptr)p), "v"(v), "i"(OFS) : "memory");
+  else atomicOr(p + OFS / 4, v);
+}
 template <uint32_t W = kWinWords>
 __device__ __forceinline__ void emit64(uint32_t* win, uint64_t acc, uint32_t len, uint32_t wp) {
   const uint64_t X = acc << ((64u - len) & 63u);  // MSB-aligned (len 0: acc is 0)
@@ -1453,9 +1465,9 @@ __device__ __forceinline__ void emit64(uint32_t* win, uint64_t acc, uint32_t len
   const uint32_t hi = (uint32_t)(X >> 32), lo = (uint32_t)X;
   if (!FC_EMIT_BRANCH) i0 = len ? i0 : (uint32_t)__lane_id();  // OR of zeros: any word, one per lane
   if (!FC_EMIT_BRANCH || len) {
-    atomicOr(&win[i0], hi >> o);
-    atomicOr(&win[i0 + 1], __builtin_amdgcn_alignbit(hi, lo, o));
-    atomicOr(&win[i0 + 2], __builtin_amdgcn_alignbit(lo, 0u, o));
+    lds_or<0>(win + i0, hi >> o);
+    lds_or<4>(win + i0, __builtin_amdgcn_alignbit(hi, lo, o));
+    lds_or<8>(win + i0, __builtin_amdgcn_alignbit(lo, 0u, o));
   }
 }
 
@@ -1467,8 +1479,8 @@ __device__ __forceinline__ void emit32(uint32_t* win, uint32_t v, uint32_t len, 
   uint32_t i0 = min(wp >> 5, W);
   if (!FC_EMIT_BRANCH) i0 = len ? i0 : (uint32_t)__lane_id();
   if (!FC_EMIT_BRANCH || len) {
-    atomicOr(&win[i0], X >> o);
-    atomicOr(&win[i0 + 1], __builtin_amdgcn_alignbit(X, 0u, o));
+    lds_or<0>(win + i0, X >> o);
+    lds_or<4>(win + i0, __builtin_amdgcn_alignbit(X, 0u, o));
   }
 }
 
@@ -1631,6 +1643,17 @@ constexpr int kWaitVm0 = 0x0F70;
 // the four ds_read_b128 that hand each lane its 16 consecutive elements are then
 // bank-conflict-free (every 16-lane group of a ds_read_b128 covers all 64 banks).
 // Only full tiles of 16-B-aligned rows are staged; returns whether it issued.
+#ifndef FC_STAGE_AUX
+#define FC_STAGE_AUX 2  // cache policy of the encoders' LDS-DMA staging loads (2: nt; the rows are read once): with FC_CODE_NT -1.3 % stochastic, -3 % uniform (profiles/r05/diag_enc_nt_ab.txt)
+#endif
+constexpr int kStageAux = FC_STAGE_AUX;
+#ifndef FC_CODE_NT
+#define FC_CODE_NT 1  // the encoders' code-word stores non-temporal (0: default policy)
+#endif
+__device__ __forceinline__ void code_store(uint32_t* p, uint32_t v) {
+  if (FC_CODE_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 __device__ __forceinline__ bool stage_tile(const EncodeArgs& a, ConstParamPtr cparams, uint32_t ticket,
                                            uint32_t* stg, int lane) {
   const int32_t t = (int32_t)div_clients(a, ticket);
@@ -1647,10 +1670,10 @@ __device__ __forceinline__ bool stage_tile(const EncodeArgs& a, ConstParamPtr cp
   const uint32_t lane_bytes = 4u * (16u * ((q - 4u * j) & 15u) + 4u * j);
   const gvptr src = (gvptr)((const char*)(x + tile_base) + lane_bytes);
   const lvptr dst = (lvptr)stg;
-  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(src, dst, 16, 1024, 0);
-  __builtin_amdgcn_global_load_lds(src, dst, 16, 2048, 0);
-  __builtin_amdgcn_global_load_lds(src, dst, 16, 3072, 0);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, kStageAux);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 1024, kStageAux);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 2048, kStageAux);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 3072, kStageAux);
   return true;
 }
 __device__ __forceinline__ int stage_pos(int lane, int j) {
@@ -2022,7 +2045,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
           const uint32_t kk = k - lead;
           const uint32_t wv32 = win_bits32(win, s0 + 32 * kk);
           if (FC_ABL & 2) asm volatile("" :: "v"(wv32));
-          else if ((int64_t)(w0 + kk + 1) * 4 <= cap) out32[w0 + kk] = bswap32(wv32);
+          else if ((int64_t)(w0 + kk + 1) * 4 <= cap) code_store(out32 + w0 + kk, bswap32(wv32));
         }
         const uint32_t nt = min((uint32_t)kWinWords, (kPre + pbody + trail_len + 31) / 32 + 1);
         if (!(FC_ABL & 1024))
@@ -2091,10 +2114,10 @@ __device__ __forceinline__ bool stage_at(const uint32_t* x, int64_t tile_base, i
   const uint32_t lane_bytes = 4u * (16u * ((q - 4u * j) & 15u) + 4u * j);
   const gvptr src = (gvptr)((const char*)(x + tile_base) + lane_bytes);
   const lvptr dst = (lvptr)stg;
-  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(src, dst, 16, 1024, 0);
-  __builtin_amdgcn_global_load_lds(src, dst, 16, 2048, 0);
-  __builtin_amdgcn_global_load_lds(src, dst, 16, 3072, 0);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, kStageAux);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 1024, kStageAux);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 2048, kStageAux);
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 3072, kStageAux);
   return true;
 }
 
@@ -2276,6 +2299,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           llen += cc.len;
           FC_CHUNK_BARRIER;
         }
+        nnz += (int32_t)__popc(lmask);  // the lane's nonzeros in this tile
         lfirst = lmask ? hrel + (int32_t)__builtin_ctz(lmask) : -1;
         llast = lmask ? hrel + 31 - (int32_t)__builtin_clz(lmask) : -1;
       } else
@@ -2466,7 +2490,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         const uint32_t kk = k - lead;
         const uint32_t wv32 = win_bits32(win, s0 + 32 * kk);
         if (FC_ABL & 2) asm volatile("" :: "v"(wv32));  // diagnostics: no stream stores
-        else if ((int64_t)(w0 + kk + 1) * 4 <= cap) out32[w0 + kk] = bswap32(wv32);
+        else if ((int64_t)(w0 + kk + 1) * 4 <= cap) code_store(out32 + w0 + kk, bswap32(wv32));
       }
       const uint32_t nt = min(kWin2Words, (kPre + body + trail_len + 31) / 32 + 1);
       for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
