@@ -1180,7 +1180,8 @@ struct ChainCode {
   uint32_t len;
   uint32_t lng;  // a code > 32 bits, |r| >= 8192 / Inf / NaN, or more than 64 bits
   uint32_t nzm;  // nonzero mask of the chunk (bit k: element k)
-  uint32_t pre;  // the chunk's first nonzero still needs its run code (a nonzero before it in the lane)
+  uint32_t pre;   // the chunk's first nonzero still needs its run code (a nonzero before it in the lane)
+  uint64_t prem;  // the wave's lanes with pre: a scalar mask across the two code paths
 };
 
 // quant_code_fast for the chained table: the same quantiser, numerics and
@@ -1280,6 +1281,7 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
     r.acc = ((uint64_t)(e0 >> 14) << l1) | (e1 >> 14);
     r.len = (e0 + e1) & 63u;  // bits 7:5 are zero: the two lengths add without interference
     r.pre = (e0 | e1) & kChainFlag;
+    r.prem = __ballot(r.pre != 0u);
     r.nzm = __builtin_amdgcn_ubfe(e0, 8, 2) | (__builtin_amdgcn_ubfe(e1, 8, 2) << 2);
     r.lng = 0;  // |q| <= 7: at most 36 bits
     return r;
@@ -1323,6 +1325,7 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
     }
     const uint32_t nzm = r.nzm;
     r.pre = (nzm != 0u && sst != 0u) ? 1u : 0u;
+    r.prem = __ballot(r.pre != 0u);
     // the state after the chunk: distance from its last nonzero to the next chunk
     const uint32_t far = kChainFar << 10;
     sst = nzm ? (4u - (31u - (uint32_t)__builtin_clz(nzm))) << 10 : (sst ? min(sst + (4u << 10), far) : 0u);
@@ -2140,12 +2143,21 @@ constexpr int kEnc2Waves = FC_ENC2_WAVES;
 template <int MODE, bool INT_IN, int DIV, bool PRE, int NT>
 __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_encode2(EncodeArgs a) {
   constexpr int STE = NT * kTE;  // elements per super-tile (ticket)
-  __shared__ uint32_t wins[kEnc2Waves][kWin2Words + 3];  // + guard words
-  __shared__ uint32_t clut[kCodeLut];
   constexpr bool CHAIN = FC_PAIR_CHAIN && FC_PAIR_LUT && !INT_IN;
   constexpr int kPL = CHAIN ? kChainLut : kPairLut;
-  __shared__ uint32_t plut[kPL];
-  __shared__ __attribute__((aligned(16))) uint32_t stgs[kEnc2Waves][kTE];  // LDS-DMA staging of the next tile
+  // one LDS block, the code tables first: their byte offsets (< 64 KiB) fold into the
+  // ds_read instruction offsets instead of an add per lookup
+  struct __attribute__((aligned(16))) Lds {
+    uint32_t plut[kPL];
+    uint32_t clut[kCodeLut];
+    uint32_t stgs[kEnc2Waves][kTE];              // LDS-DMA staging of the next tile
+    uint32_t wins[kEnc2Waves][kWin2Words + 3];  // + guard words
+  };
+  __shared__ Lds lds;
+  uint32_t* const plut = lds.plut;
+  uint32_t* const clut = lds.clut;
+  auto& stgs = lds.stgs;
+  auto& wins = lds.wins;
   for (int i = threadIdx.x; i < kCodeLut; i += kEncThreads * kEnc2Waves) clut[i] = code_lut_entry((uint32_t)i);
   for (int i = threadIdx.x; i < kPL; i += kEncThreads * kEnc2Waves)
     plut[i] = CHAIN ? pair_chain_entry((uint32_t)i) : pair_lut_entry((uint32_t)i);
@@ -2283,7 +2295,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
                 (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - lrel - 4 * j)));
           else
             cc = quant_code_chain<MODE, DIV, PRE>(cq, g, raw[j], dist, nnz, clut, plut, sst);
-          if (__ballot(cc.pre != 0u) != 0) {
+          if (cc.prem != 0) {
             if (cc.pre) {  // a nonzero before it in the lane: lmask != 0
               const uint32_t d = 4u * (uint32_t)j + (uint32_t)__builtin_ctz(cc.nzm) - (31u - (uint32_t)__builtin_clz(lmask));
               const uint32_t rl = 63u - 2u * (uint32_t)__builtin_clz(d);  // glen(d)
