@@ -1175,6 +1175,35 @@ __device__ __forceinline__ uint32_t pair_chain_entry(uint32_t i) {
   return (code << 14) | (flag << 13) | (run << 10) | (nzp << 8) | len;
 }
 
+// The super-tile encoder's distortion sum.  FC_DIST_MFMA: each element slot's
+// squared errors added by one v_mfma_f32_16x16x4_f32 with the errors as both
+// operands -- its diagonal D[i][i] gathers sum_k dd(lane 16k + i)^2, so the
+// diagonal's total is the wave's sum -- on the matrix pipe instead of one VALU
+// FMA per element (the wave total is read off the diagonal once per ticket).
+#ifndef FC_DIST_MFMA
+#define FC_DIST_MFMA 0  // measured: +17 % stochastic, +4 % uniform (the dependent MFMA chain stalls the wave; profiles/r05/diag_enc_dist_mfma_ab.txt)
+#endif
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+struct DistAcc {
+  float s;
+  f32x4_t m;
+  __device__ __forceinline__ void zero() {
+    s = 0.0f;
+    m = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+  }
+  __device__ __forceinline__ void add(float dd) {
+    if (FC_DIST_MFMA) m = __builtin_amdgcn_mfma_f32_16x16x4f32(dd, dd, m, 0, 0, 0);
+    else s = fmaf(dd, dd, s);
+  }
+  // the wave's total (every lane); D[i][j] sits in lane j + 16 (i / 4), register i % 4
+  __device__ __forceinline__ float wave_total(int lane) const {
+    if (!FC_DIST_MFMA) return wave_sum_f(s);
+    const int a = lane & 15, b = lane >> 4;
+    const float d = (a & 3) == 0 ? m.x : (a & 3) == 1 ? m.y : (a & 3) == 2 ? m.z : m.w;
+    return wave_sum_f((a >> 2) == b ? d : 0.0f);
+  }
+};
+
 struct ChainCode {
   uint64_t acc;
   uint32_t len;
@@ -1193,7 +1222,7 @@ struct ChainCode {
 constexpr bool PK = FC_PK;
 template <int MODE, int DIV, bool PRE, bool MASK = false>
 __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_t g, const uint32_t (&r4)[4],
-                                                      float& dist, int32_t& nnz, const uint32_t* clut,
+                                                      DistAcc& dist, const uint32_t* clut,
                                                       const uint32_t* plut, uint32_t& sst, int32_t nvalid = 4) {
   // r.nzm: the chunk's nonzero mask (the caller counts the lane's nonzeros from the
   // masks once per tile); on the pair-table path it comes from the table entries, so
@@ -1237,9 +1266,10 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
       r23 = f2{u23v.x <= p23.x ? ceilf(sc[2]) : fl23.x, u23v.y <= p23.y ? ceilf(sc[3]) : fl23.y};
     }
     const f2 dd01 = sc01 - r01, dd23 = sc23 - r23;
-    f2 dv = dd01 * dd01;
-    dv = __builtin_elementwise_fma(dd23, dd23, dv);
-    dist += dv.x + dv.y;
+    dist.add(dd01.x);
+    dist.add(dd01.y);
+    dist.add(dd23.x);
+    dist.add(dd23.y);
     q[0] = r01.x; q[1] = r01.y; q[2] = r23.x; q[3] = r23.y;
   } else {
 #pragma unroll
@@ -1259,7 +1289,7 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
     }
     const float rq = (MODE == FC_DITHERED) ? (r + noise) : r;
     const float dd = DIV == 1 ? sc - rq : xv - rq * cq.step;
-    dist = (!MASK || k < nvalid) ? fmaf(dd, dd, dist) : dist;
+    dist.add((!MASK || k < nvalid) ? dd : 0.0f);
     q[k] = r;
   }
   }
@@ -2206,6 +2236,8 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     uint32_t ntk = 0;
     uint64_t pw1 = 0, pw2 = 0;  // look-back window (lane i: super-tile t2-64+i); 0: not fetched
     float dist = 0.0f;
+    DistAcc dacc;  // (the chained-table path)
+    dacc.zero();
     int32_t nnz = 0;  // INT_IN and CHAIN: per lane; else the wave total
     uint32_t lng = 0;  // lane has a long chunk (either tile)
     uint32_t body = 0;
@@ -2291,10 +2323,10 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           ChainCode cc;
           if (MODE == FC_DITHERED && !full)
             cc = quant_code_chain<MODE, DIV, PRE, true>(
-                cq, g, raw[j], dist, nnz, clut, plut, sst,
+                cq, g, raw[j], dacc, clut, plut, sst,
                 (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - lrel - 4 * j)));
           else
-            cc = quant_code_chain<MODE, DIV, PRE>(cq, g, raw[j], dist, nnz, clut, plut, sst);
+            cc = quant_code_chain<MODE, DIV, PRE>(cq, g, raw[j], dacc, clut, plut, sst);
           if (cc.prem != 0) {
             if (cc.pre) {  // a nonzero before it in the lane: lmask != 0
               const uint32_t d = 4u * (uint32_t)j + (uint32_t)__builtin_ctz(cc.nzm) - (31u - (uint32_t)__builtin_clz(lmask));
@@ -2397,7 +2429,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     STAMP(4);
     // fast path: no long chunk, prefix + body + trailing code + one funnel word fit
     // the window, and a finite distortion (no NaN / infinite r)
-    const float dsum = INT_IN ? 0.0f : wave_sum_f(dist);
+    const float dsum = INT_IN ? 0.0f : CHAIN ? dacc.wave_total(lane) : wave_sum_f(dist);
     const bool fast = __ballot(lng != 0) == 0 && kPre + body + 96u <= 32u * kWin2Words &&
                       (INT_IN || dsum <= 3.4028235e38f);
     uint64_t* const status_f = FC_FRESH_ARGS >= 2 ? enc_args_fresh().status : a.status;
