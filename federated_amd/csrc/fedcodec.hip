@@ -4096,6 +4096,16 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // FC_NORM_L2_LINF: one pass for both wrapper norms, norms[c] = ||x||_2 and
 // norms[C + c] = max |x| (builder.py:100-117: clipping and zeroing).
 constexpr int kNormThreads = 1024;
+// Row reads of the streaming reducers (k_client_norms, k_mask_encode): each byte is
+// read once, FC_ROW_NT 1 issues them non-temporal.
+#ifndef FC_ROW_NT
+#define FC_ROW_NT 1  // one-bit 128 x 25 M encode -8 %, client norms -2 %, 1024 x 25 one-bit within noise (profiles/r05/diag_row_nt_ab.txt)
+#endif
+typedef float f4row_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4row_t ld_row4(const __attribute__((address_space(1))) f4row_t* p) {
+  if (FC_ROW_NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
 // Client split (few clients per GPU): client c's tiles are cut into gridDim.x
 // parts, part s = [s ntile / S, (s + 1) ntile / S), one workgroup each, so a
 // GPU's share of 64-128 clients still fills every CU.  Each part writes its
@@ -4133,7 +4143,7 @@ __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* cons
     f4v raw[8];
     if (full) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) raw[k] = *(gf4ptr)(xg + base + 256 * k + 4 * lane);
+      for (int k = 0; k < 8; ++k) raw[k] = ld_row4((gf4ptr)(xg + base + 256 * k + 4 * lane));
     } else {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -4307,7 +4317,7 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
     const int64_t base = tile * 2048;
     if (base + 2048 <= P && aligned) {  // wave-uniform: 8 float4 loads, no branches
 #pragma unroll
-      for (int k = 0; k < 8; ++k) raw[k] = *(gf4ptr)(xg + base + 256 * k + 4 * lane);
+      for (int k = 0; k < 8; ++k) raw[k] = ld_row4((gf4ptr)(xg + base + 256 * k + 4 * lane));
     } else {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
