@@ -29,3 +29,41 @@ def _super_tiles(monkeypatch, request):
   the exact path, so the denser cases here also take the exact re-encode)."""
   monkeypatch.setenv("FEDCODEC_ENC2", "1")
   monkeypatch.setenv("FEDCODEC_ENC_NT", request.param)
+
+
+@pytest.mark.parametrize("pattern", ["last", "first", "edges", "one_late"])
+def test_super_tile_edge_positions(gpu, pattern):
+  """Nonzeros only at a super-tile's first / last element (eight-tile tickets: relative
+  positions 0 and 8191, where round 4's 13-bit fields held their "no nonzero" mark),
+  over 64 super-tiles per client: the aggregates the look-back combines carry those
+  positions, and the code, index and sum stay the oracle's."""
+  import numpy as np
+  import torch
+  from federated_amd import _lib, codec
+  from oracle import codec as ocodec
+  from oracle import quantize_utils as oq
+  ste = 8 * 1024
+  P, C = 64 * ste + 5, 6
+  xs = []
+  for c in range(C):
+    x = np.zeros(P, np.float32)
+    if pattern in ("last", "edges"):
+      x[ste - 1::ste] = 1.0 + c
+    if pattern in ("first", "edges"):
+      x[0::ste] = -2.0
+    if pattern == "one_late":  # one nonzero, far into the row: every other aggregate is empty
+      x[40 * ste + ste - 1] = 3.0
+    xs.append(x)
+  seeds = np.array([[c, c] for c in range(C)], np.int64)
+  batch = codec.quantize_encode_checked([torch.from_numpy(x).to(gpu) for x in xs], 0.5,
+                                        torch.from_numpy(seeds), _lib.UNIFORM)
+  acc = np.zeros(P, np.int64)
+  for c in range(C):
+    q = oq.uniform_quantize(xs[c], 0.5)
+    code, nbits = ocodec.run_length_gamma_encode(q)
+    assert batch.bits()[c] == nbits
+    assert batch.client_code(c) == code
+    acc += q
+  s, _, err = codec.decode_accumulate(batch)
+  assert int(err.item()) == 0
+  np.testing.assert_array_equal(s.cpu().numpy(), acc.astype(np.int32))
