@@ -2129,6 +2129,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
 #define FC_WIN2_WORDS (FC_PAIR_CHAIN ? (FC_ENC2_WAVES == 8 ? 1240 : 952) : 2 * FC_WIN_WORDS)
 #endif
 constexpr uint32_t kWin2Words = FC_WIN2_WORDS;
+static_assert(kWin2Words % 4 == 0, "k_encode2 zeroes its window 16 bytes at a time");
 // NT-tile tickets while codes are expected within this many bits per element: a
 // window holds 32 * kWin2Words - kPre - 96 bits (1240 words: ~9.6 bits per element
 // for four tiles, ~4.8 for eight); the host's expectation is the caller's
@@ -2181,7 +2182,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
     uint32_t plut[kPL];
     uint32_t clut[kCodeLut];
     uint32_t stgs[kEnc2Waves][kTE];              // LDS-DMA staging of the next tile
-    uint32_t wins[kEnc2Waves][kWin2Words + 3];  // + guard words
+    uint32_t wins[kEnc2Waves][kWin2Words + 4];  // + guard words (rows 16-byte aligned)
   };
   __shared__ Lds lds;
   uint32_t* const plut = lds.plut;
@@ -2195,7 +2196,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
   const int lane = (int)(threadIdx.x & 63u);
   uint32_t* win = wins[wave];
   uint32_t* stg = stgs[wave];
-  for (int i = lane; i < (int)kWin2Words + 3; i += kEncThreads) win[i] = 0;
+  for (int i = lane; i < (int)kWin2Words + 4; i += kEncThreads) win[i] = 0;
   __syncthreads();
   const uint32_t total = (uint32_t)a.nclients * (uint32_t)a.T2;
   const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
@@ -2529,15 +2530,24 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&enc_args_fresh().overflow[c], 1u);
       const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
       const uint32_t lead = kStoreAlign ? (uint32_t)(((uintptr_t)(out32 + w0) >> 2) & 31u) : 0u;  // lanes before the line
-      for (uint32_t k = lane; k < nwords_owned + lead; k += kEncThreads) {
+      // the words inside the stream's capacity (a client that overflows is re-encoded by
+      // the caller), counted once; word kk = window bits [s0 + 32 kk, +32): a funnel of
+      // window words (s0 >> 5) + kk and + 1 by the ticket-uniform s0 & 31
+      const uint32_t nst = (uint32_t)max<int64_t>(0, min<int64_t>(nwords_owned, cap / 4 - (int64_t)w0));
+      const uint32_t so = s0 & 31u;
+      const uint32_t* const wsrc = win + (s0 >> 5);
+      uint32_t* const dst = out32 + w0;
+      for (uint32_t k = lane; k < nst + lead; k += kEncThreads) {
         if (k < lead) continue;
         const uint32_t kk = k - lead;
-        const uint32_t wv32 = win_bits32(win, s0 + 32 * kk);
+        const uint32_t a0 = wsrc[kk], a1 = wsrc[kk + 1];
+        const uint32_t wv32 = so ? __builtin_amdgcn_alignbit(a0, a1, 32u - so) : a0;
         if (FC_ABL & 2) asm volatile("" :: "v"(wv32));  // diagnostics: no stream stores
-        else if ((int64_t)(w0 + kk + 1) * 4 <= cap) code_store(out32 + w0 + kk, bswap32(wv32));
+        else code_store(dst + kk, bswap32(wv32));
       }
-      const uint32_t nt = min(kWin2Words, (kPre + body + trail_len + 31) / 32 + 1);
-      for (uint32_t i = lane; i < nt; i += kEncThreads) win[i] = 0;
+      // the dirtied window words back to zero, 16 bytes per lane and instruction
+      const uint32_t nt4 = (min(kWin2Words, (kPre + body + trail_len + 31) / 32 + 1) + 3u) & ~3u;
+      for (uint32_t i = 4 * lane; i < nt4; i += 4 * kEncThreads) *(uint4*)(win + i) = make_uint4(0u, 0u, 0u, 0u);
     }
     ticket = ticket1;
     if (ticket1 < total) ticket1 = shard + a.nshards * uniform(ntk);
