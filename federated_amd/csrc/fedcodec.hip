@@ -2072,13 +2072,19 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         if (lane == 0 && (int64_t)(w0 + nwords_owned) * 4 > cap) atomicOr((uint32_t*)&enc_args_fresh().overflow[pc], 1u);
         const uint32_t s0 = kPre - bstart;  // window bit of stream-window bit 0
         const uint32_t lead = kStoreAlign ? (uint32_t)(((uintptr_t)(out32 + w0) >> 2) & 31u) : 0u;  // lanes before the line
+        // (as k_encode2: the capacity bound once, a tile-uniform funnel per word)
+        const uint32_t nst = (uint32_t)max<int64_t>(0, min<int64_t>(nwords_owned, cap / 4 - (int64_t)w0));
+        const uint32_t so = s0 & 31u;
+        const uint32_t* const wsrc = win + (s0 >> 5);
+        uint32_t* const dst = out32 + w0;
         if (!(FC_ABL & 1024))
-        for (uint32_t k = lane; k < nwords_owned + lead; k += kEncThreads) {
+        for (uint32_t k = lane; k < nst + lead; k += kEncThreads) {
           if (k < lead) continue;
           const uint32_t kk = k - lead;
-          const uint32_t wv32 = win_bits32(win, s0 + 32 * kk);
+          const uint32_t a0 = wsrc[kk], a1 = wsrc[kk + 1];
+          const uint32_t wv32 = so ? __builtin_amdgcn_alignbit(a0, a1, 32u - so) : a0;
           if (FC_ABL & 2) asm volatile("" :: "v"(wv32));
-          else if ((int64_t)(w0 + kk + 1) * 4 <= cap) code_store(out32 + w0 + kk, bswap32(wv32));
+          else code_store(dst + kk, bswap32(wv32));
         }
         const uint32_t nt = min((uint32_t)kWinWords, (kPre + pbody + trail_len + 31) / 32 + 1);
         if (!(FC_ABL & 1024))
