@@ -2171,6 +2171,12 @@ constexpr int kEnc2Waves = FC_ENC2_WAVES;
 #ifndef FC_LB_LATE
 #define FC_LB_LATE 0  // k_encode2: look-back window loaded after the last tile's codes (A/B knob)
 #endif
+#ifndef FC_SCAN_SKIP
+#define FC_SCAN_SKIP 1  // k_encode2: no max-scan for the lanes' previous nonzero when every lane has one (-0.6 %)
+#endif
+#ifndef FC_RUN_MERGE
+#define FC_RUN_MERGE 1  // k_encode2: the lane's run code emitted with its first chunk pair when they fit 64 bits (-1.2 %; both -1.4 %, profiles/r05/diag_enc_scan_merge_ab.txt)
+#endif
 #ifndef FC_FRESH_ARGS
 #define FC_FRESH_ARGS 0  // k_encode2's once-per-ticket fields re-read from the kernel arguments: 0 none,
                          // 1 partials + index pointers, 2 also the status pointer and T2 (A/B knob:
@@ -2394,9 +2400,17 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       }
       // ---- B: scans -- last nonzero before each lane (lane 0: the first half's
       //      last nonzero, or none), then code offsets after the bits so far
-      const int32_t im = dpp_incl_max(max(llast, slast));  // slast < every position of this tile
-      const int32_t lprev = dpp_shr1(im, slast);
-      const int32_t hlast = lane63(im);
+      int32_t lprev, hlast;
+      if (FC_SCAN_SKIP && __ballot(lfirst < 0) == 0) {
+        // every lane holds a nonzero (dense tiles): the lanes' last nonzeros already rise
+        // with the lane, so the one before lane l is lane l - 1's (lane 0: slast)
+        lprev = dpp_shr1(llast, slast);
+        hlast = lane63(llast);
+      } else {
+        const int32_t im = dpp_incl_max(max(llast, slast));  // slast < every position of this tile
+        lprev = dpp_shr1(im, slast);
+        hlast = lane63(im);
+      }
       const bool lrun = lfirst >= 0 && lprev >= 0;
       const uint32_t dv = lrun ? (uint32_t)(lfirst - lprev) : 0u;
       const uint32_t R = lrun ? glen(dv) : 0u;
@@ -2406,6 +2420,15 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
       // ---- C: emit the lane's run code and chunks
       if (!(FC_ABL & 1)) {  // (diagnostics: no emission)
         uint32_t o = kPre + body + is - ltot;
+        if (FC_RUN_MERGE && __ballot(R + clen[0] + clen[1] > 64u || clen[2] + clen[3] > 64u) == 0) {
+          // the run code and the chunk pairs fit 64 bits across the wave (the common
+          // case): two pieces, the run code leading the first
+          const uint32_t c01 = clen[0] + clen[1];
+          const uint64_t a01 = ((uint64_t)dv << (c01 & 63u)) | (cacc[0] << (clen[1] & 63u)) | cacc[1];
+          const uint64_t a23 = (cacc[2] << (clen[3] & 63u)) | cacc[3];
+          emit64<kWin2Words>(win, a01, R + c01, o);
+          emit64<kWin2Words>(win, a23, clen[2] + clen[3], o + R + c01);
+        } else {
         emit32<kWin2Words>(win, dv, R, o);
         o += R;
         if (__ballot(clen[0] + clen[1] > 64u || clen[2] + clen[3] > 64u) == 0) {
@@ -2420,6 +2443,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
             emit64<kWin2Words>(win, cacc[j], clen[j], o);
             o += clen[j];
           }
+        }
         }
       }
       if (sfirst < 0) {
