@@ -1221,12 +1221,10 @@ struct ChainCode {
 #endif
 constexpr bool PK = FC_PK;
 template <int MODE, int DIV, bool PRE, bool MASK = false>
-__device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_t g, const uint32_t (&r4)[4],
-                                                      DistAcc& dist, const uint32_t* clut,
-                                                      const uint32_t* plut, uint32_t& sst, int32_t nvalid = 4) {
-  // r.nzm: the chunk's nonzero mask (the caller counts the lane's nonzeros from the
-  // masks once per tile); on the pair-table path it comes from the table entries, so
-  // no per-element compares are issued there
+__device__ __forceinline__ void quant_chain4(const ClientQ& cq, uint32_t g, const uint32_t (&r4)[4], DistAcc& dist,
+                                             float (&q)[4], int32_t nvalid = 4) {
+  // Philox + the exact quantiser + the distortion terms of one chunk (its codes:
+  // code_chain)
   uint4 rb = make_uint4(0, 0, 0, 0);
   if (FC_ABL & 8) {
     rb.x = g * 2654435761u; rb.y = rb.x ^ 0x9E3779B9u; rb.z = rb.x + cq.key.k0; rb.w = rb.y ^ cq.key.k1;
@@ -1234,7 +1232,6 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
     rb = philox_group_u(cq.key, g);
   }
   const uint32_t rbits[4] = {rb.x, rb.y, rb.z, rb.w};
-  float q[4];
   if (PK && DIV == 1 && !MASK && MODE != FC_DITHERED) {
     // the same arithmetic with the elementwise multiplies, subtractions and the
     // distortion terms as packed float32 pairs (v_pk_mul / v_pk_add / v_pk_fma_f32:
@@ -1293,12 +1290,23 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
     q[k] = r;
   }
   }
+}
+
+// The codes of one chunk from its quantised values (the chained pair table when
+// |q| <= 7 across the wave -- TAB: the caller has checked that for the whole tile --
+// else the code table / exponent paths); sst carries the run state.
+template <bool TAB = false>
+__device__ __forceinline__ ChainCode code_chain(const float (&q)[4], const uint32_t* clut, const uint32_t* plut,
+                                                uint32_t& sst) {
+  // r.nzm: the chunk's nonzero mask (the caller counts the lane's nonzeros from the
+  // masks once per tile); on the pair-table path it comes from the table entries, so
+  // no per-element compares are issued there
   ChainCode r;
   const float mabs = vmax3_abs(q[0], q[1], vmax3_abs(q[2], q[3], 0.0f));
   const bool bad = !(mabs < 8192.0f);
   r.acc = 0;
   r.len = 0;
-  if (__ballot(!(mabs <= 7.0f)) == 0) {
+  if (TAB || __ballot(!(mabs <= 7.0f)) == 0) {
     // |q| <= 7 across the wave: two chained pair-table reads
     // 1.5 * 2^23 + 4 qa + 64 qb is an exact float integer whose low 10 bits are
     // 4 * ((qa + 16 qb) mod 256): the pair's byte offset in a state region
@@ -1362,6 +1370,15 @@ __device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_
   }
   r.lng = (bad || r.len > 64u) ? 1u : 0u;
   return r;
+}
+
+template <int MODE, int DIV, bool PRE, bool MASK = false>
+__device__ __forceinline__ ChainCode quant_code_chain(const ClientQ& cq, uint32_t g, const uint32_t (&r4)[4],
+                                                      DistAcc& dist, const uint32_t* clut,
+                                                      const uint32_t* plut, uint32_t& sst, int32_t nvalid = 4) {
+  float q[4];
+  quant_chain4<MODE, DIV, PRE, MASK>(cq, g, r4, dist, q, nvalid);
+  return code_chain(q, clut, plut, sst);
 }
 
 // Re-read and re-quantise one chunk (slow path: tiles with codes > 32 bits or
@@ -1490,11 +1507,11 @@ __device__ __forceinline__ void lds_or(uint32_t* p, uint32_t v) {
   if (FC_EMIT_ASM) asm volatile("ds_or_b32 %0, %1 offset:%2" ::"v"((lds_uptr)p), "v"(v), "i"(OFS) : "memory");
   else atomicOr(p + OFS / 4, v);
 }
-template <uint32_t W = kWinWords>
+template <uint32_t W = kWinWords, bool CLAMP = true>  // CLAMP false: the caller keeps wp inside the window
 __device__ __forceinline__ void emit64(uint32_t* win, uint64_t acc, uint32_t len, uint32_t wp) {
   const uint64_t X = acc << ((64u - len) & 63u);  // MSB-aligned (len 0: acc is 0)
   const uint32_t o = wp & 31u;
-  uint32_t i0 = min(wp >> 5, W);
+  uint32_t i0 = CLAMP ? min(wp >> 5, W) : wp >> 5;
   const uint32_t hi = (uint32_t)(X >> 32), lo = (uint32_t)X;
   if (!FC_EMIT_BRANCH) i0 = len ? i0 : (uint32_t)__lane_id();  // OR of zeros: any word, one per lane
   if (!FC_EMIT_BRANCH || len) {
@@ -1505,11 +1522,11 @@ __device__ __forceinline__ void emit64(uint32_t* win, uint64_t acc, uint32_t len
 }
 
 // Same for a code of len <= 32 bits: two ds_or_b32.
-template <uint32_t W = kWinWords>
+template <uint32_t W = kWinWords, bool CLAMP = true>
 __device__ __forceinline__ void emit32(uint32_t* win, uint32_t v, uint32_t len, uint32_t wp) {
   const uint32_t X = (uint32_t)((uint64_t)v << ((32u - len) & 63u));  // MSB-aligned (len 0: v is 0)
   const uint32_t o = wp & 31u;
-  uint32_t i0 = min(wp >> 5, W);
+  uint32_t i0 = CLAMP ? min(wp >> 5, W) : wp >> 5;
   if (!FC_EMIT_BRANCH) i0 = len ? i0 : (uint32_t)__lane_id();
   if (!FC_EMIT_BRANCH || len) {
     lds_or<0>(win + i0, X >> o);
@@ -2171,6 +2188,9 @@ constexpr int kEnc2Waves = FC_ENC2_WAVES;
 #ifndef FC_LB_LATE
 #define FC_LB_LATE 0  // k_encode2: look-back window loaded after the last tile's codes (A/B knob)
 #endif
+#ifndef FC_QUANT_FIRST
+#define FC_QUANT_FIRST 0  // k_encode2: a tile's chunks quantised before any is coded (measured even: profiles/r05/diag_enc_qfirst_ab.txt)
+#endif
 #ifndef FC_SCAN_SKIP
 #define FC_SCAN_SKIP 1  // k_encode2: no max-scan for the lanes' previous nonzero when every lane has one (-0.6 %)
 #endif
@@ -2330,11 +2350,25 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
         // run state across the lane's chunks: only a far run (or a chunk off the
         // pair table) needs its first run code prepended, from the lane's mask
         uint32_t sst = 0, lmask = 0;
+        // FC_QUANT_FIRST: the tile's four chunks quantised first (four independent Philox
+        // chains in one straight block), one |q| <= 7 test for the tile, then the codes
+        float qv[kChunks][4];
+        bool tab = false;
+        if (FC_QUANT_FIRST && !(MODE == FC_DITHERED && !full)) {
+#pragma unroll
+          for (int j = 0; j < kChunks; ++j) quant_chain4<MODE, DIV, PRE>(cq, gbase + (uint32_t)j, raw[j], dacc, qv[j]);
+          float m = 0.0f;
+#pragma unroll
+          for (int j = 0; j < kChunks; ++j) m = vmax3_abs(qv[j][0], qv[j][1], vmax3_abs(qv[j][2], qv[j][3], m));
+          tab = __ballot(!(m <= 7.0f)) == 0;
+        }
 #pragma unroll
         for (int j = 0; j < kChunks; ++j) {
           const uint32_t g = gbase + (uint32_t)j;
           ChainCode cc;
-          if (MODE == FC_DITHERED && !full)
+          if (FC_QUANT_FIRST && !(MODE == FC_DITHERED && !full))
+            cc = tab ? code_chain<true>(qv[j], clut, plut, sst) : code_chain(qv[j], clut, plut, sst);
+          else if (MODE == FC_DITHERED && !full)
             cc = quant_code_chain<MODE, DIV, PRE, true>(
                 cq, g, raw[j], dacc, clut, plut, sst,
                 (int32_t)min<int64_t>(4, max<int64_t>(0, P - tile_base - lrel - 4 * j)));
