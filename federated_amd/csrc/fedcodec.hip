@@ -2853,6 +2853,9 @@ constexpr int kDecChunk = FC_DEC_CHUNK;  // 16-byte blocks per chunk (one 64-B l
 #ifndef FC_DEC_LONG
 #define FC_DEC_LONG 4
 #endif
+#ifndef FC_DEC_UNROLL
+#define FC_DEC_UNROLL 1  // decode_segment's loop unrolled by the batch interval: headline decode -1 %, config 2 -4 % (profiles/r05/diag_dec_unroll_ab.txt)
+#endif
 #ifndef FC_DEC_LONG_LANES
 #define FC_DEC_LONG_LANES 16  // waiting lanes that trigger an arithmetic slot before its turn
 #endif
@@ -3155,7 +3158,12 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
   const uint32_t lo_addr = my_addr, hi_addr = my_addr + 4u * span;
   uint32_t bad = 0;
   uint32_t it = 0;
-  while (cons < total) {
+  // one iteration; K: its place in an unrolled group of kDecBatch (FC_DEC_UNROLL: the batch
+  // points and arithmetic slots at fixed places, no iteration count through the
+  // divergent loop), else the count `it`
+  auto iter = [&](auto kpos) -> bool {
+    constexpr int K = decltype(kpos)::value;
+    constexpr bool UNR = K >= 0;
 #ifdef FC_STAMPS
     {  // diagnostics (tools/diag/dec_diverge.py): wave iterations, one count per iteration the wave runs
       const uint64_t ex = __ballot(1);
@@ -3164,8 +3172,8 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
 #endif
     // every active lane is on the same iteration: a wave-uniform count (the scalar unit
     // keeps it, not three VALU per iteration where the loop's exit is divergent)
-    it = __builtin_amdgcn_readfirstlane(it + 1u);
-    if ((it & (kDecBatch - 1)) == 0) r.batch();
+    if (!UNR) it = __builtin_amdgcn_readfirstlane(it + 1u);
+    if (UNR ? K == kDecBatch - 1 : (it & (kDecBatch - 1)) == 0) r.batch();
 #if FC_DEC_ABL & 16  // diagnostics: 12 extra independent VALU per iteration (is the loop issue-bound?)
     {
       uint32_t p0 = it, p1 = it + 1, p2 = it + 2, p3 = it + 3;
@@ -3255,7 +3263,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       }
     }
     if (!tdone && idle && (!R1 || u == 0 || fill - cons > 32) &&
-        (LONG || (it & (kDecLong - 1)) == 0 ||
+        (LONG || (UNR ? K == kDecLong - 1 : (it & (kDecLong - 1)) == 0) ||
          (FC_DEC_LONG_LANES <= 64 && __popcll(__ballot(idle)) >= FC_DEC_LONG_LANES))) {
       // right after a refill (>= 33 window bits): one code decoded arithmetically
       const uint32_t top = (uint32_t)(r.win >> 32);
@@ -3304,7 +3312,19 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       fill += 32;
     }
     }
-    if (stop) break;
+    return stop;
+  };
+  if (FC_DEC_UNROLL) {
+    static_assert(!FC_DEC_UNROLL || (kDecBatch == 4 && kDecLong == 4), "unrolled by four");
+    while (cons < total) {
+      if (iter(std::integral_constant<int, 0>{}) || !(cons < total)) break;
+      if (iter(std::integral_constant<int, 1>{}) || !(cons < total)) break;
+      if (iter(std::integral_constant<int, 2>{}) || !(cons < total)) break;
+      if (iter(std::integral_constant<int, 3>{})) break;
+    }
+  } else {
+    while (cons < total)
+      if (iter(std::integral_constant<int, -1>{})) break;
   }
   // the reader's last batch-point load may still be in flight into its register
   // tuple: land it before the tuple dies (the registers are reused after the segment)
