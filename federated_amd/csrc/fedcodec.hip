@@ -3707,14 +3707,17 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
   bool failed = false;
   int nk = 0;  // (!EMIT, ckp) checkpoints recorded
   int32_t ckt = ckp ? a.ckb : INT32_MAX;  // the next checkpoint's threshold (past the last: never)
-  while (cons < lim) {
+  // one iteration (as decode_segment: FC_DEC_UNROLL places the batch points by position)
+  auto iter = [&](auto kpos) -> bool {
+    constexpr int K = decltype(kpos)::value;
+    constexpr bool UNR = K >= 0;
     if (!EMIT && cons >= ckt) {  // a code start: checkpoint
       ckp[nk * ckst] = (uint64_t)cons | ((uint64_t)(nsum + (acc4 >> 2)) << 13);
       ++nk;
       ckt = nk < a.nck ? (nk + 1) * a.ckb : INT32_MAX;
     }
-    it = __builtin_amdgcn_readfirstlane(it + 1u);
-    if ((it & (kDecBatch - 1)) == 0) r.batch();
+    if (!UNR) it = __builtin_amdgcn_readfirstlane(it + 1u);
+    if (UNR ? K == kDecBatch - 1 : (it & (kDecBatch - 1)) == 0) r.batch();
     const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
     const uint32_t Ls = e >> 26;
     const int32_t dd4 = (int32_t)((e & 0x7Fu) + ((e >> 7) & 0x7Fu));
@@ -3766,7 +3769,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
       bool took = false;
       if (EMIT && L == a.P - 1) {  // every element covered: the code ends here, no trailing run
         end->bend = end->total = p;
-        break;
+        return true;
       }
       if (z1 <= 15u && z2 <= 15u && Lw <= 32u && cons + (int32_t)Lw <= avail && (!EMIT || L + (int64_t)d < a.P)) {
         r.win <<= Lw;
@@ -3780,12 +3783,12 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
         if (EMIT) {
           if (!d || L + (int64_t)d > a.P) {
             end->bad = true;
-            break;
+            return true;
           }
           if (L + (int64_t)d == a.P) {  // the trailing zero run
             end->bend = p;
             end->total = ir.pos;
-            break;
+            return true;
           }
         }
         bool ok = d != 0u;
@@ -3800,7 +3803,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
         if (!ok) {
           if (EMIT) end->bad = true;
           failed = true;
-          break;
+          return true;
         }
         cons = (int32_t)(ir.pos - start);
         fill = restart(cons);
@@ -3811,17 +3814,29 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
         for (; u < nu && (u << gs) <= nz; ++u) idx_put(a, c, u, en);
         L = nz;
         room4 = room_of(L);
-        if (u > u_stop) break;  // the entries asked for are written
+        if (u > u_stop) return true;  // the entries asked for are written
       } else {
         nsum += d;
       }
-      if (!took) continue;  // the window restarted full
+      if (!took) return false;  // the window restarted full
     }
     if (fill - cons <= 32) {  // (the blocks are zero past the code's end)
       const uint32_t wd = r.pop32();
       r.win |= (uint64_t)wd << (32 - (fill - cons));
       fill += 32;
     }
+    return false;
+  };
+  if (FC_DEC_UNROLL) {
+    while (cons < lim) {
+      if (iter(std::integral_constant<int, 0>{}) || !(cons < lim)) break;
+      if (iter(std::integral_constant<int, 1>{}) || !(cons < lim)) break;
+      if (iter(std::integral_constant<int, 2>{}) || !(cons < lim)) break;
+      if (iter(std::integral_constant<int, 3>{})) break;
+    }
+  } else {
+    while (cons < lim)
+      if (iter(std::integral_constant<int, -1>{})) break;
   }
   r.wait_nxt();  // (async) the last batch-point load lands before its registers are reused
   if (!EMIT && ckp)
