@@ -4012,6 +4012,12 @@ __global__ __launch_bounds__(64) void k_idx_scan(IdxArgs a) {
 #ifndef FC_IDX_EMIT_WPE
 #define FC_IDX_EMIT_WPE 4  // 6 or 8 (64-80 VGPRs) spill in the parse: 56 / 50 ms vs 38.5 at the headline
 #endif
+#ifndef FC_IDX_CK_CARRY
+#define FC_IDX_CK_CARRY 1  // the emit's checkpoint scan carried over a lane's units (0: rescanned per unit)
+#endif
+#ifndef FC_IDX_CKW
+#define FC_IDX_CKW 4  // checkpoint loads in flight per scan step
+#endif
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX_EMIT_WPE))) void k_idx_emit(IdxArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t lut[kLutSize];
   idx_load_lut(lut);
@@ -4041,9 +4047,49 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX
     const int64_t ulast = ckd ? Lnext >> gs : u;
     int64_t cp = s, cl = L;
     bool bad = false;
+#if FC_IDX_CK_CARRY
+    // the checkpoints rise in position and runs, and so do the unit bounds: the scan
+    // carries over the lane's units (each checkpoint read once), FC_IDX_CKW loads in
+    // flight; the latest one before the bound is the parse start if past the meeting
+    int kc = ckd ? 0 : a.nck;       // checkpoints [0, kc) lie before an earlier bound
+    int64_t kpos = -1, klk = 0;     // the latest of them (-1: none)
+#endif
     while (u <= ulast) {
       const int64_t bound = u << gs;
       int64_t ps = cp, pl = cl;
+#if FC_IDX_CK_CARRY
+      while (kc < a.nck) {
+        uint64_t e[FC_IDX_CKW];
+#pragma unroll
+        for (int i = 0; i < FC_IDX_CKW; ++i) e[i] = a.ck[(int64_t)min(kc + i, a.nck - 1) * lanes + g];
+        int n = 0;
+        bool stop = false;
+#pragma unroll
+        for (int i = 0; i < FC_IDX_CKW; ++i) {
+          if (stop || kc + i >= a.nck) {
+            stop = true;
+          } else if (e[i] == kCkNone) {
+            n = a.nck - kc;  // none after it either
+            stop = true;
+          } else {
+            const int64_t lk = adj + (int64_t)(e[i] >> 13);
+            if (lk >= bound) {
+              stop = true;
+            } else {
+              kpos = cb + (int64_t)(e[i] & 0x1FFFu);
+              klk = lk;
+              n = i + 1;
+            }
+          }
+        }
+        kc += n;
+        if (stop) break;
+      }
+      if (kpos >= m && kpos > ps) {
+        ps = kpos;
+        pl = klk;
+      }
+#else
       for (int k = 0; ckd && k < a.nck; ++k) {
         const uint64_t e = a.ck[k * lanes + g];
         if (e == kCkNone) break;
@@ -4055,6 +4101,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(FC_IDX
           pl = lk;
         }
       }
+#endif
       const IdxLock r = idx_parse<true>(a, c, lut, ps, ce, pl, &end, nullptr, 0, ckd ? u : INT64_MAX);
       if (!ckd) {
         if (end.bad) {
