@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 ZZ (final build, after the rebuild unroll): full GPU suite, smoke, the bench line, then rocprofv3 records of
+# round-5 ZZ (final build: rebuild unroll + carried emit checkpoint scan): full GPU suite, smoke, the bench line, then rocprofv3 records of
 # the workloads this round's last changes touched
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
