@@ -6040,8 +6040,13 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   const bool virt = !plane && a.vidx_main != nullptr;  // an unstitched segmented batch
   const bool qtr = !plane && !virt && a.idxq != nullptr;  // quarter-tile lane segments
   int span = (!plane && !qtr && nclients >= kDecSpan2Clients) ? 2 : 1;
-  if (const char* e = getenv("FEDCODEC_DEC_SPAN")) span = (!plane && !qtr && atoi(e) == 2) ? 2 : 1;  // test knob
-  int lpt = span == 2 ? 256 : 128;
+  if (const char* e = getenv("FEDCODEC_DEC_SPAN")) {  // test knob: 1, 2 or 4 tiles per lane segment
+    const int v = atoi(e);
+    // (an unstitched segmented batch: at most two, so a lane segment straddles at most one
+    // encoder segment's end)
+    span = (plane || qtr) ? 1 : v == 4 ? (virt ? 2 : 4) : v == 2 ? 2 : 1;
+  }
+  int lpt = span >= 2 ? 256 : 128;
   while (lpt > 64 && lpt / 2 >= nclients) lpt /= 2;
   if (const char* l = getenv("FEDCODEC_DEC_LPT")) {  // test knob: lanes per tile (64, 128 or 256)
     const int v = atoi(l);
@@ -6051,7 +6056,7 @@ int decode_common(DecodeArgs a, const uint8_t* stream_buf, const int64_t* stream
   void (*kern)(DecodeArgs) = plane  ? (a.plane8 ? k_decode<2> : k_decode<1>)
                              : qtr  ? k_decode<0, 1, true>
                              : virt ? (span == 2 ? k_decode<0, 2, false, true> : k_decode<0, 1, false, true>)
-                             : span == 2 ? k_decode<0, 2> : k_decode<0, 1>;
+                             : span == 4 ? k_decode<0, 4> : span == 2 ? k_decode<0, 2> : k_decode<0, 1>;
   const int ue = qtr ? kTE / 4 : kTE;  // elements per unit
   const int tpw = kDecThreads / lpt * span;  // units per workgroup
   const int repl = qtr ? FC_DEC_QTR_REPL : FC_DEC_REPL;

@@ -1,8 +1,8 @@
-"""The decoder's parity tests again with two-tile lane segments (k_decode<false, 2>).
+"""The decoder's parity tests again with two- and four-tile lane segments (k_decode<false, 2 / 4>).
 
 The launcher takes two-tile segments (256 lanes per tile pair) only from 256
 clients on; these small-batch tests would otherwise run one-tile segments.
-FEDCODEC_DEC_SPAN=2 forces them: every rlgamma shape (P = 1 .. 100,003: a single
+FEDCODEC_DEC_SPAN=2 (or 4, the four-tile knob) forces them: every rlgamma shape (P = 1 .. 100,003: a single
 partial tile, odd tile counts, a last segment of one tile), each rounding's
 batch round, tile-range decodes starting and ending at odd tiles (the
 multi-GPU slabs), malformed streams, the golden rounds and the config rounds.
@@ -20,6 +20,6 @@ from test_gpu_configs import test_config_round_matches_oracle  # noqa: F401
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _two_tile_segments(monkeypatch):
-  monkeypatch.setenv("FEDCODEC_DEC_SPAN", "2")
+@pytest.fixture(autouse=True, params=["2", "4"])
+def _multi_tile_segments(request, monkeypatch):
+  monkeypatch.setenv("FEDCODEC_DEC_SPAN", request.param)
