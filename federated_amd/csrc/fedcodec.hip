@@ -4434,8 +4434,18 @@ __device__ __forceinline__ uint32_t dpp_row_shl(uint32_t x, int n) {
 // writes its sums to part[c][s] = {S1, S2, A1, A2, count}; k_mask_finalize adds
 // the parts in order and forms the means and the distortion.
 constexpr int kObPart = 5;  // doubles per part
+#ifndef FC_OB_F32X
+#define FC_OB_F32X 0  // sums of x (and of x over the mask) in float32 tile partials (A/B knob; 0: float64)
+#endif
+#ifndef FC_OB_WPE
+#define FC_OB_WPE 0  // waves per SIMD the mask encoder's registers are held to (0: the compiler's choice)
+#endif
 template <int KIND>
-__global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* xs, int64_t P, float thr,
+__global__ __launch_bounds__(kObThreads)
+#if FC_OB_WPE
+__attribute__((amdgpu_waves_per_eu(FC_OB_WPE)))
+#endif
+void k_mask_encode(const float* const* xs, int64_t P, float thr,
                                                             uint32_t* masks, double* part) {
   __shared__ double red[4][kObWaves];
   __shared__ uint64_t redn[kObWaves];
@@ -4450,10 +4460,10 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
   part_range(ntile, (int)blockIdx.x, (int)gridDim.x, tlo, thi);
   const bool aligned = ((uintptr_t)x & 15u) == 0;
   // KIND 0: s1 = sum x, s2 = sum x^2, a1 / a2 = the same over x >= thr;
-  // KIND 1: s1 = sum |x|, s2 = sum x^2.  Sums of x: float32 partials over a
-  // tile's 32 elements per lane, float64 across tiles; sums of squares in float64
-  // throughout (x^2 exact: the distortion below subtracts nearly equal terms).
-  // Fixed order everywhere.
+  // KIND 1: s1 = sum |x|, s2 = sum x^2.  Sums of x in float64 (FC_OB_F32X: float32
+  // partials over a tile's 32 elements per lane, float64 across tiles); sums of
+  // squares in float64 throughout (x^2 exact: the distortion below subtracts nearly
+  // equal terms).  Fixed order everywhere.
   double s1 = 0.0, s2 = 0.0, a1 = 0.0, a2 = 0.0;
   uint32_t na = 0;
   // clients start at different tiles: rows share their alignment, and reading
@@ -4488,7 +4498,8 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
   auto do_tile = [&](int64_t tile, const f4v (&raw)[8]) {
     const int64_t base = tile * 2048;
     const bool full = base + 2048 <= P;
-    double p1[2] = {0.0, 0.0}, q1[2] = {0.0, 0.0};  // two chains each
+    typedef __typeof__(FC_OB_F32X ? 0.0f : 0.0) xsum_t;  // the sums of x per tile
+    xsum_t p1[2] = {0, 0}, q1[2] = {0, 0};  // two chains each
     double p2[2] = {0.0, 0.0}, q2[2] = {0.0, 0.0};
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -4504,13 +4515,23 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
         nib |= ab ? (1u << i) : 0u;
         const double vd = (double)v;
         if (KIND == 0) {
-          p1[k & 1] += vd;
-          p2[k & 1] = fma(vd, vd, p2[k & 1]);
-          const double td = ab ? vd : 0.0;
-          q1[k & 1] += td;
-          q2[k & 1] = fma(td, td, q2[k & 1]);
+          if (FC_OB_F32X) {
+            const float tf = ab ? v : 0.0f;
+            p1[k & 1] += v;
+            q1[k & 1] += tf;
+            const double td = (double)tf;
+            p2[k & 1] = fma(vd, vd, p2[k & 1]);
+            q2[k & 1] = fma(td, td, q2[k & 1]);
+          } else {
+            p1[k & 1] += vd;
+            p2[k & 1] = fma(vd, vd, p2[k & 1]);
+            const double td = ab ? vd : 0.0;
+            q1[k & 1] += td;
+            q2[k & 1] = fma(td, td, q2[k & 1]);
+          }
         } else {
-          p1[k & 1] += fabs(vd);
+          if (FC_OB_F32X) p1[k & 1] += fabsf(v);
+          else p1[k & 1] += fabs(vd);
           p2[k & 1] = fma(vd, vd, p2[k & 1]);
         }
       }
@@ -4521,26 +4542,38 @@ __global__ __launch_bounds__(kObThreads) void k_mask_encode(const float* const* 
       wd |= dpp_row_shl(wd, 4) << 16;
       if ((lane & 7) == 0) wordbuf[wv][8 * k + (lane >> 3)] = wd;
     }
-    s1 += p1[0] + p1[1];
+    s1 += (double)(p1[0] + p1[1]);
     s2 += p2[0] + p2[1];
     if (KIND == 0) {
-      a1 += q1[0] + q1[1];
+      a1 += (double)(q1[0] + q1[1]);
       a2 += q2[0] + q2[1];
     }
     __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses execute in order
     const uint32_t word = wordbuf[wv][lane];
     if (tile * 64 + lane < nw) m[tile * 64 + lane] = word;
   };
-  // software-pipelined: the next tile's loads are in flight while a tile computes
-  f4v ra[8], rb[8];
-  if (tlo + wv < thi) load_tile(tile_of(tlo + wv), ra);
-  for (int64_t tt = tlo + wv; tt < thi; tt += 2 * kObWaves) {
-    const int64_t tn = tt + kObWaves;
-    if (tn < thi) load_tile(tile_of(tn), rb);
-    do_tile(tile_of(tt), ra);
-    if (tn >= thi) break;
-    if (tn + kObWaves < thi) load_tile(tile_of(tn + kObWaves), ra);
-    do_tile(tile_of(tn), rb);
+#ifndef FC_OB_PIPE
+#define FC_OB_PIPE 1  // the next tile's loads in flight while a tile computes (0: one tile per wave at a time)
+#endif
+  if (FC_OB_PIPE) {
+    // software-pipelined: the next tile's loads are in flight while a tile computes
+    f4v ra[8], rb[8];
+    if (tlo + wv < thi) load_tile(tile_of(tlo + wv), ra);
+    for (int64_t tt = tlo + wv; tt < thi; tt += 2 * kObWaves) {
+      const int64_t tn = tt + kObWaves;
+      if (tn < thi) load_tile(tile_of(tn), rb);
+      do_tile(tile_of(tt), ra);
+      if (tn >= thi) break;
+      if (tn + kObWaves < thi) load_tile(tile_of(tn + kObWaves), ra);
+      do_tile(tile_of(tn), rb);
+    }
+  } else {
+    // one tile per wave at a time, fewer registers: more waves keep more bytes in flight
+    for (int64_t tt = tlo + wv; tt < thi; tt += kObWaves) {
+      f4v ra[8];
+      load_tile(tile_of(tt), ra);
+      do_tile(tile_of(tt), ra);
+    }
   }
   // fixed-order reductions: lanes (shuffle tree), then waves in order
   s1 = wave_sum_f64(s1);
