@@ -494,11 +494,11 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 24)) {  // safety net only: tickets guarantee progress
+        // (a timed-out look-back never yields a prefix: the caller re-encodes the client --
+        // k_encode_exact's callers through the overflow flag)
         if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
-        k = 0;
-        w1 = kFlagPre;
-        w2 = kFlagPre;
-        break;
+        slow = true;
+        return S;
       }
     }
     // fold lanes k (farthest, or 63) .. 0 (nearest) serially in scalar registers
@@ -563,11 +563,10 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
       const uint64_t need = pre ? ~0ull << (63 - (int)__clzll(pre)) : ~0ull;
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {
+      if (++spins > (1u << 24)) {  // (safety net) the client goes to the exact path
         if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
         Seg r = seg_identity();
-        r.has_nz = 1;
-        r.first = r.last = -1;
+        r.has_nz = kSegSlow;
         return r;
       }
       if (!valid) {
@@ -707,12 +706,10 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     if ((val & need) == need) break;
     FC_COUNT(9, 1);
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1u << 24)) {
+    if (++spins > (1u << 24)) {  // (safety net) the client goes to the exact path
       if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
-      Seg r = seg_identity();
-      r.has_nz = 1;
-      r.first = r.last = -1;
-      return r;
+      slow = true;
+      return seg_identity();
     }
     if (!valid) {
       const uint64_t w1 = ld_agent(status_c + 2 * (int64_t)ti);
@@ -2703,6 +2700,9 @@ __global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
       }
       bool slow = false;
       excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, slow);
+      // (only a timed-out look-back: every status here is the exact kernel's own) the
+      // client's code is unusable; its overflow flag makes the checked caller re-encode it
+      if (slow && lane == 0) atomicOr((uint32_t*)&enc_args_fresh().overflow[c], 1u);
     }
     const Seg incl = seg_combine(excl, agg);
     SlowEmit e;
