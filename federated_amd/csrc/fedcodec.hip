@@ -3080,20 +3080,29 @@ constexpr uint32_t gen_entry(uint32_t i) {
 // The decode tables, computed at compile time; each k_decode workgroup copies them
 // into LDS with 16-byte loads instead of building them (measured even: config 2's
 // decode 0.239 -> 0.238 ms, the builds overlapped other workgroups' decoding).
+// The index parse (fc_build_index) needs only a step's bits and its runs: ilut keeps
+// L in [29:26] and 4 (d1 + d2) in [7:0], so the runs come out with one AND.
+#ifndef FC_IDX_ILUT
+#define FC_IDX_ILUT 1  // the index parse reads ilut (0: the decoder's table, two fields added per step)
+#endif
 struct DecTabs {
   uint32_t lut[kLutSize];
   uint16_t glut[kLutSize];
+  uint32_t ilut[kLutSize];
 };
 constexpr DecTabs make_dec_tabs() {
   DecTabs t{};
   for (uint32_t i = 0; i < (uint32_t)kLutSize; ++i) {
-    t.lut[i] = lut_entry(i);
+    const uint32_t e = lut_entry(i);
+    t.lut[i] = e;
     t.glut[i] = (uint16_t)gen_entry(i);
+    t.ilut[i] = (e & (15u << 26)) | ((e & 0x7Fu) + ((e >> 7) & 0x7Fu));
   }
   return t;
 }
 __device__ const DecTabs g_dec_tabs = make_dec_tabs();
-static_assert(sizeof(DecTabs) % 16 == 0 && offsetof(DecTabs, glut) % 16 == 0, "16-byte table copies");
+static_assert(sizeof(DecTabs) % 16 == 0 && offsetof(DecTabs, glut) % 16 == 0 && offsetof(DecTabs, ilut) % 16 == 0,
+              "16-byte table copies");
 
 constexpr int kDecThreads = 256;
 // Tiles per lane segment (accumulator path), chosen per launch: two with 256
@@ -3668,6 +3677,11 @@ struct IdxEnd {
   int64_t bend, total;  // bend >= 0: the code ended in this chunk
   bool bad;
 };
+// 4 x the runs of a table step's codes (ilut: one field; the decoder's table: two)
+__device__ __forceinline__ int32_t idx_runs4(uint32_t e) {
+  return FC_IDX_ILUT ? (int32_t)(e & 0xFFu) : (int32_t)((e & 0x7Fu) + ((e >> 7) & 0x7Fu));
+}
+
 template <bool EMIT>
 __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const uint32_t* lut, int64_t start,
                                              int64_t stop, int64_t L, IdxEnd* end, uint64_t* ckp = nullptr,
@@ -3720,7 +3734,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
     if (UNR ? K == kDecBatch - 1 : (it & (kDecBatch - 1)) == 0) r.batch();
     const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
     const uint32_t Ls = e >> 26;
-    const int32_t dd4 = (int32_t)((e & 0x7Fu) + ((e >> 7) & 0x7Fu));
+    const int32_t dd4 = idx_runs4(e);
     const int32_t lend = min(lim, avail);  // a table step's codes must end inside both
     bool stepped = false;
     if (!EMIT && FC_IDX_UNIFORM && __ballot(cons + 2 * kLutBits > lend) == 0) {
@@ -3734,7 +3748,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
       const uint32_t L2 = e2 >> 26;
       r.win <<= L2;
       cons += (int32_t)L2;
-      acc4 += (int32_t)((e2 & 0x7Fu) + ((e2 >> 7) & 0x7Fu));
+      acc4 += idx_runs4(e2);
       stepped = Ls != 0u;
     } else if (Ls != 0u && cons + (int32_t)Ls <= lend && (!EMIT || acc4 + dd4 < room4)) {
       r.win <<= Ls;
@@ -3744,7 +3758,7 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
       // iteration looks at the same bits again
       const uint32_t e2 = lut[(uint32_t)(r.win >> (64 - kLutBits))];
       const uint32_t L2 = e2 >> 26;
-      const int32_t d24 = (int32_t)((e2 & 0x7Fu) + ((e2 >> 7) & 0x7Fu));
+      const int32_t d24 = idx_runs4(e2);
       if (L2 != 0u && cons + (int32_t)L2 <= lend && (!EMIT || acc4 + d24 < room4)) {
         r.win <<= L2;
         cons += (int32_t)L2;
@@ -3861,7 +3875,8 @@ __device__ __forceinline__ IdxLock idx_parse(const IdxArgs& a, int64_t c, const 
 
 // The decode table in LDS for a workgroup of chunk lanes (persistent grids).
 __device__ __forceinline__ void idx_load_lut(uint32_t* lut) {
-  for (int i = threadIdx.x; i < kLutSize / 4; i += blockDim.x) ((uint4*)lut)[i] = ((const uint4*)g_dec_tabs.lut)[i];
+  const uint4* src = (const uint4*)(FC_IDX_ILUT ? g_dec_tabs.ilut : g_dec_tabs.lut);
+  for (int i = threadIdx.x; i < kLutSize / 4; i += blockDim.x) ((uint4*)lut)[i] = src[i];
   __syncthreads();
 }
 
