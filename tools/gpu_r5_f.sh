@@ -1,14 +1,14 @@
 #!/bin/bash
-# round-5 F: k_encode2 knob A/B on one box -- v0: no scalar round-2 xor, no fresh
-# arguments; v1: + round-2 xor; v2: + partials / index pointers re-read; current: +
-# status pointer and T2 re-read.  Then the streaming floor with one / two tiles in flight.
+# round-5 F (final build: + look-back timeout handling, index-parse table, decoder span knob, mask-encoder knobs): full GPU suite, smoke, the bench line, then rocprofv3 records
+# the workloads this round's last changes touched
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-export TMPDIR=/tmp
-for m in 1 1 0; do
-  for v in _v0 _v1 _v2 ""; do
-    FEDCODEC_LIB=$PWD/federated_amd/libfedcodec$v.so CAP=0.6 MODE=$m REPS=5 DEC=0 timeout -k 10 200 python3 tools/enc_bench.py >> gpurun_out/r5f_enc.txt 2>&1 || exit 2
-  done
-done
-timeout -k 10 200 python3 tools/floor_bench.py > gpurun_out/r5f_floor.txt 2>&1 || exit 3
-FEDCODEC_FLOOR_DEPTH=2 timeout -k 10 200 python3 tools/floor_bench.py > gpurun_out/r5f_floor_d2.txt 2>&1 || exit 4
+rm -rf gpurun_out/prof10
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r5f_tests.txt 2>&1 || { tail -30 gpurun_out/r5f_tests.txt; exit 1; }
+tail -1 gpurun_out/r5f_tests.txt
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5f_smoke.txt 2>&1 || { tail -20 gpurun_out/r5f_smoke.txt; exit 1; }
+tail -1 gpurun_out/r5f_smoke.txt
+timeout -k 10 900 python3 bench.py > gpurun_out/r5f_bench.json 2> gpurun_out/r5f_bench.err || { tail -20 gpurun_out/r5f_bench.err; exit 1; }
+head -c 300 gpurun_out/r5f_bench.json; echo
+timeout -k 10 1000 bash tools/profile_workloads.sh gpurun_out/prof10 bare_decode headline > gpurun_out/r5f_prof.log 2>&1 || { tail -5 gpurun_out/r5f_prof.log; exit 1; }
+tail -1 gpurun_out/r5f_prof.log
