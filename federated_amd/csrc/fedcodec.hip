@@ -494,11 +494,15 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 24)) {  // safety net only: tickets guarantee progress
-        // (a timed-out look-back never yields a prefix: the caller re-encodes the client --
-        // k_encode_exact's callers through the overflow flag)
+        // (a timed-out look-back's fold is not a prefix: `slow` makes the caller re-encode the
+        // client -- k_encode_exact's callers through the overflow flag; the fold itself runs on,
+        // which keeps this cold path from changing the encoders' register allocation)
         if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
         slow = true;
-        return S;
+        k = 0;
+        w1 = kFlagPre;
+        w2 = kFlagPre;
+        break;
       }
     }
     // fold lanes k (farthest, or 63) .. 0 (nearest) serially in scalar registers
