@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 F (final build: + look-back timeout handling, index-parse table, decoder span knob, mask-encoder knobs): full GPU suite, smoke, the bench line, then rocprofv3 records
+# round-5 F (final build: look-back timeout flag-only, index-parse table, decoder span knob, mask-encoder knobs): full GPU suite, smoke, the bench line, then rocprofv3 records
 # the workloads this round's last changes touched
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
