@@ -5767,6 +5767,9 @@ __device__ __forceinline__ uint32_t code_bits(uint32_t code, uint32_t len, uint3
 // common case) they are a funnel shift of 5 source words and one 16-byte store;
 // otherwise each word is gathered from the (usually one or two) pieces it spans.
 // Bits past the client's last bit are zero, as the encoder's owner-written last word.
+#ifndef FC_SEG_NT
+#define FC_SEG_NT 0  // the stitch's segment reads and stream stores non-temporal (A/B knob)
+#endif
 constexpr int kSegGroups = 4;                      // 16-byte groups per thread per item
 constexpr int kSegWordsPerBlock = 1024 * kSegGroups;  // words per (client, item)
 __device__ __forceinline__ uint32_t seg_word(const SegPlan* pl, int nseg, int64_t total, int64_t w, int& k) {
@@ -5839,7 +5842,7 @@ __global__ __launch_bounds__(256) void k_seg_copy(SegArgs a, int64_t blocks_per_
         const uint32_t* s32 = (const uint32_t*)e.src + (sb >> 5);
         sh[g] = (uint32_t)(sb & 31);
 #pragma unroll
-        for (int j = 0; j < 5; ++j) x[g][j] = s32[j];
+        for (int j = 0; j < 5; ++j) x[g][j] = FC_SEG_NT ? __builtin_nontemporal_load(s32 + j) : s32[j];
         fast |= 1u << g;
       }
     }
@@ -5858,7 +5861,12 @@ __global__ __launch_bounds__(256) void k_seg_copy(SegArgs a, int64_t blocks_per_
         v.y = bswap32(o ? (y[1] << o) | (y[2] >> (32 - o)) : y[1]);
         v.z = bswap32(o ? (y[2] << o) | (y[3] >> (32 - o)) : y[2]);
         v.w = bswap32(o ? (y[3] << o) | (y[4] >> (32 - o)) : y[3]);
-        *(uint4*)(out32 + w) = v;
+        if (FC_SEG_NT) {
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (u32x4*)(out32 + w));
+        } else {
+          *(uint4*)(out32 + w) = v;
+        }
       } else {
         for (int64_t ww = max(w, wstart); ww < min(nwords, w + 4); ++ww) {
           const uint32_t v = seg_word(pl, a.nseg, total, ww, k);
