@@ -3089,10 +3089,18 @@ constexpr uint32_t gen_entry(uint32_t i) {
 #ifndef FC_IDX_ILUT
 #define FC_IDX_ILUT 1  // the index parse reads ilut (0: the decoder's table, two fields added per step)
 #endif
+// FC_DEC_TAB2: the decoder's table steps read byte fields (4 d1, 4 d2, v1, v2 as int8:
+// byte selects and one arithmetic shift instead of bit-field extracts) from dlut and
+// the bits consumed from a separate byte table llut (A/B knob).
+#ifndef FC_DEC_TAB2
+#define FC_DEC_TAB2 0
+#endif
 struct DecTabs {
   uint32_t lut[kLutSize];
   uint16_t glut[kLutSize];
   uint32_t ilut[kLutSize];
+  uint32_t dlut[kLutSize];
+  uint8_t llut[kLutSize];
 };
 constexpr DecTabs make_dec_tabs() {
   DecTabs t{};
@@ -3101,11 +3109,17 @@ constexpr DecTabs make_dec_tabs() {
     t.lut[i] = e;
     t.glut[i] = (uint16_t)gen_entry(i);
     t.ilut[i] = (e & (15u << 26)) | ((e & 0x7Fu) + ((e >> 7) & 0x7Fu));
+    // 6-bit two's complement values widened to int8 bytes
+    const uint32_t v1 = (e >> 14) & 63u, v2 = (e >> 20) & 63u;
+    const uint32_t b1 = v1 >= 32u ? v1 | 0xC0u : v1, b2 = v2 >= 32u ? v2 | 0xC0u : v2;
+    t.dlut[i] = (e & 0x7Fu) | (((e >> 7) & 0x7Fu) << 8) | (b1 << 16) | (b2 << 24);
+    t.llut[i] = (uint8_t)(e >> 26);
   }
   return t;
 }
 __device__ const DecTabs g_dec_tabs = make_dec_tabs();
-static_assert(sizeof(DecTabs) % 16 == 0 && offsetof(DecTabs, glut) % 16 == 0 && offsetof(DecTabs, ilut) % 16 == 0,
+static_assert(sizeof(DecTabs) % 16 == 0 && offsetof(DecTabs, glut) % 16 == 0 && offsetof(DecTabs, ilut) % 16 == 0 &&
+                  offsetof(DecTabs, dlut) % 16 == 0 && offsetof(DecTabs, llut) % 16 == 0,
               "16-byte table copies");
 
 constexpr int kDecThreads = 256;
@@ -3159,7 +3173,7 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
                                                uint64_t b1, int32_t rel, uint32_t my_addr,
                                                const uint32_t* lut, int32_t* err, int32_t* ptile,
                                                uint32_t hib, uint32_t span = kTE,
-                                               const uint16_t* glut = nullptr) {
+                                               const uint16_t* glut = nullptr, const uint8_t* llut = nullptr) {
   SegReader r;
   const int32_t total = (int32_t)(b1 - b0);
   r.init(base, cap, b0, total);
@@ -3212,12 +3226,22 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
     for (int st = 0; st < (LONG ? 0 : 2); ++st) {  // table steps (the window holds >= 33 bits when they start)
       // the window is zero past the segment end (the client's next tile): no table
       // entry takes a code there
-      const uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
-      relb += e & 0x7Fu;
-      acc_add_at<PLANE>(relb, ((int32_t)(e << 12)) >> 26, ptile, hib, err);
-      relb += (e >> 7) & 0x7Fu;
-      acc_add_at<PLANE>(relb, ((int32_t)(e << 6)) >> 26, ptile, hib, err);
-      const uint32_t L = e >> 26;
+      const uint32_t ix = (uint32_t)(r.win >> (64 - kLutBits));
+      const uint32_t e = lut[ix];
+      uint32_t L;
+      if (FC_DEC_TAB2) {
+        L = llut[ix];
+        relb += e & 0xFFu;
+        acc_add_at<PLANE>(relb, ((int32_t)(e << 8)) >> 24, ptile, hib, err);
+        relb += (e >> 8) & 0xFFu;
+        acc_add_at<PLANE>(relb, ((int32_t)e) >> 24, ptile, hib, err);
+      } else {
+        relb += e & 0x7Fu;
+        acc_add_at<PLANE>(relb, ((int32_t)(e << 12)) >> 26, ptile, hib, err);
+        relb += (e >> 7) & 0x7Fu;
+        acc_add_at<PLANE>(relb, ((int32_t)(e << 6)) >> 26, ptile, hib, err);
+        L = e >> 26;
+      }
       r.win <<= L;
       cons += (int32_t)L;
       if (st == 0) moved = L;  // a zero first step leaves the window as it was: so does the second
@@ -3226,13 +3250,23 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       // a third table step where the window still holds 13 or more valid bits (so
       // the refill below restores >= 33); otherwise an empty entry
       const bool ok3 = fill - cons >= kLutBits + 1;
-      uint32_t e = lut[(uint32_t)(r.win >> (64 - kLutBits))];
+      const uint32_t ix = (uint32_t)(r.win >> (64 - kLutBits));
+      uint32_t e = lut[ix];
       e = ok3 ? e : 0u;
-      relb += e & 0x7Fu;
-      acc_add_at<PLANE>(relb, ((int32_t)(e << 12)) >> 26, ptile, hib, err);
-      relb += (e >> 7) & 0x7Fu;
-      acc_add_at<PLANE>(relb, ((int32_t)(e << 6)) >> 26, ptile, hib, err);
-      const uint32_t L = e >> 26;
+      uint32_t L;
+      if (FC_DEC_TAB2) {
+        L = ok3 ? (uint32_t)llut[ix] : 0u;
+        relb += e & 0xFFu;
+        acc_add_at<PLANE>(relb, ((int32_t)(e << 8)) >> 24, ptile, hib, err);
+        relb += (e >> 8) & 0xFFu;
+        acc_add_at<PLANE>(relb, ((int32_t)e) >> 24, ptile, hib, err);
+      } else {
+        relb += e & 0x7Fu;
+        acc_add_at<PLANE>(relb, ((int32_t)(e << 12)) >> 26, ptile, hib, err);
+        relb += (e >> 7) & 0x7Fu;
+        acc_add_at<PLANE>(relb, ((int32_t)(e << 6)) >> 26, ptile, hib, err);
+        L = e >> 26;
+      }
       r.win <<= L;
       cons += (int32_t)L;
     }
@@ -3371,6 +3405,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
   // where 8-bit steps occur); the other variants keep their LDS for occupancy
   constexpr bool GEN = FC_DEC_GEN && QTR && !PLANE;
   __shared__ __attribute__((aligned(16))) uint16_t glut[GEN ? kLutSize : 8];
+  __shared__ __attribute__((aligned(16))) uint8_t llut[FC_DEC_TAB2 ? kLutSize : 16];
   extern __shared__ int32_t acc[];     // [units_per_wg][UE] sums
   // a lane's segment: SPAN consecutive units of one client (the accumulator path)
   constexpr int SPAN = PLANE ? 1 : SPAN_;
@@ -3378,7 +3413,10 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
   constexpr int UPT = kTE / UE;            // units per tile
   const int tid = threadIdx.x;
   const int units_per_wg = kDecThreads / a.lanes_per_tile * SPAN;
-  for (int i = tid; i < kLutSize / 4; i += kDecThreads) ((uint4*)lut)[i] = ((const uint4*)g_dec_tabs.lut)[i];
+  for (int i = tid; i < kLutSize / 4; i += kDecThreads)
+    ((uint4*)lut)[i] = ((const uint4*)(FC_DEC_TAB2 ? g_dec_tabs.dlut : g_dec_tabs.lut))[i];
+  if (FC_DEC_TAB2)
+    for (int i = tid; i < kLutSize / 16; i += kDecThreads) ((uint4*)llut)[i] = ((const uint4*)g_dec_tabs.llut)[i];
   if (GEN)
     for (int i = tid; i < kLutSize / 8; i += kDecThreads) ((uint4*)glut)[i] = ((const uint4*)g_dec_tabs.glut)[i];
   const int sub = tid / a.lanes_per_tile;
@@ -3471,12 +3509,13 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(QTR
         // a wave whose segments are all long-code streams skips the table steps
         if (kDecLongBits > 0 && __ballot(bend - bstart < (uint64_t)kDecLongBits * span) == 0)
           decode_segment<PLANE, true, false, GEN>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err,
-                                                  ptile, hib, span, glut);
+                                                  ptile, hib, span, glut, llut);
         else if (kDecStep3Bits16 > 0 && __ballot(bend - bstart >= (uint64_t)kDecStep3Bits16 * (span / 16)) == 0)
           decode_segment<PLANE, false, true>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err, ptile,
-                                             hib, span);
+                                             hib, span, nullptr, llut);
         else
-          decode_segment<PLANE>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err, ptile, hib, span);
+          decode_segment<PLANE>(a.stream_buf + soff, scap, bstart, bend, rel, paddr, lut, a.err, ptile, hib, span,
+                                nullptr, llut);
       }
       }  // pieces
     }
