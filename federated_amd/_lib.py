@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get("FEDCODEC_LIB") or os.path.join(_HERE, "libfedcodec.so
 UNIFORM, STOCHASTIC, DITHERED = 0, 1, 2
 NORM_MEAN_MAGNITUDE, NORM_MAX_MAGNITUDE, NORM_DIMENSIONLESS, NORM_L2, NORM_LINF, NORM_L2_LINF = 1, 2, 3, 4, 5, 6
 TILE_ELEMS = 1024
+OVERFLOW_CAPACITY, OVERFLOW_STALL = 1, 2  # FC_OVERFLOW_* bits of the encoders' overflow[]
 MAX_ELEMS = (1 << 30) - (1 << 26)  # FC_MAX_ELEMS: one client tensor
 MAX_ROW_ELEMS = (1 << 26) - 1  # FC_MAX_ROW_ELEMS: one encoder row (longer tensors are segmented)
 
@@ -58,6 +59,7 @@ SIGNATURES = {
     "fc_vote_lengths": (_INT, [_P, _I32, _I64, _P, _I32, _P, _INT, _P, _P, _P, _I64, _P]),
     "fc_dequantize": (_INT, [_P, _I64, _F32, _P, _P, _P]),
     "fc_copy": (_INT, [_P, _P, _I64, _P]),
+    "fc_diag_occupy": (_INT, [ctypes.c_uint32, _I64, _P, _P]),
     "fc_quantize_floor": (_INT, [_P, _I32, _I64, _F32, _P, _INT, _P, _P, _P, _I64, _P]),
     "fc_noise_sum": (_INT, [_P, _I32, _I64, _P, _P]),
     "fc_client_norms": (_INT, [_P, _I32, _I64, _INT, _P, _P]),

@@ -5,6 +5,8 @@ round's batch of client deltas (``fc_quantize_encode``), one call decodes and
 sums them (``fc_decode_accumulate``).  All buffers stay in HBM; the only host
 syncs are the overflow check and the small per-client measurement vectors.
 """
+import warnings
+
 import numpy as np
 import torch
 
@@ -61,6 +63,7 @@ class EncodedBatch:
     self.seg = None
     self._seg_ws = None
     self._pending = None
+    self.stalled = np.zeros(0, np.int64)  # clients whose encode stalled (check_overflow)
 
   def join(self, stream=None):
     """Order `stream` (default: the current one) after a pending stitch."""
@@ -500,9 +503,23 @@ def quantize_encode(xs, step, seeds, mode, norms=None, caps=None, stream=None, p
   return out
 
 
+class EncoderStallWarning(RuntimeWarning):
+  """An encoder look-back polled past its spin limit (FC_OVERFLOW_STALL): the
+  clients named were re-encoded on the exact path, so their codes are correct, but
+  the launch lost progress (DESIGN.md §2 "Ticket streams and progress")."""
+
+
 def check_overflow(batch):
-  """Host check; returns indices of clients whose capacity was too small."""
-  return np.nonzero(batch.overflow.cpu().numpy())[0]
+  """Host check (one copy of the flags): returns the indices of clients whose
+  capacity was too small (FC_OVERFLOW_CAPACITY).  Clients whose encode stalled
+  (FC_OVERFLOW_STALL) are kept in ``batch.stalled`` and reported as an
+  EncoderStallWarning (the tests turn it into an error)."""
+  flags = batch.overflow.cpu().numpy()
+  batch.stalled = np.nonzero(flags & _lib.OVERFLOW_STALL)[0]
+  if len(batch.stalled):
+    warnings.warn("encoder look-back hit its spin limit; clients %s were re-encoded on the exact path"
+                  % batch.stalled.tolist(), EncoderStallWarning, stacklevel=2)
+  return np.nonzero(flags & _lib.OVERFLOW_CAPACITY)[0]
 
 
 def quantize_encode_checked(xs, step, seeds, mode, norms=None, caps=None, prescale=None, segments=None):

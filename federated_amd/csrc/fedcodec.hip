@@ -57,20 +57,25 @@ constexpr uint32_t kNoPos = 0x3FFF; // "no nonzero" in a 14-bit (super-)tile-rel
 // (MI355X_MICROARCH.md "dequeue"), so tickets come from kTicketShards counters,
 // one 64-B line each; stream k hands out tickets k, k + K, k + 2K, ... in order.
 constexpr int kTicketShards = 32;
-#ifndef FC_XCD_SHARD
-#define FC_XCD_SHARD 0  // measured neutral (profiles/r04/diag_xcd_streams.txt): off
-#endif
-// Ticket stream of wave w of workgroup b.  XCD groups (workgroups are dealt
-// round-robin over the 8 XCDs, so b % 8 names the group; speed only): stream
-// k is drawn by one group's waves only (k % 8 == b % 8), so with the client
-// count a multiple of 8 -- client = ticket mod C -- every tile of a client is
-// coded on one XCD and the partial lines its tickets share (the code words
-// at ticket boundaries, the per-tile index / distortion / nonzero slots,
-// statuses) merge in that XCD's L2 instead of being written back once per XCD.
-__device__ __forceinline__ uint32_t ticket_shard(uint32_t b, uint32_t w, uint32_t wpg, uint32_t nshards,
-                                                 uint32_t xcd) {
-  if (xcd) return (b & 7u) + 8u * (((b >> 3) * wpg + w) % (nshards >> 3));
-  return (b * wpg + w) % nshards;
+// A wave draws from stream (r mod K), r = its START ORDER (a per-launch counter every
+// wave increments once when it begins), not from its blockIdx.  Progress: the
+// smallest ticket m nobody has taken belongs to stream s; every wave of stream s
+// holds only tickets below m, whose predecessors are all taken, so (by induction on
+// m) they finish and one of them takes m -- provided stream s has a wave that has
+// started.  With start-order streams the first K waves that start cover all K
+// streams, and a started wave stays resident until its stream is exhausted, so any
+// K co-resident waves suffice (two wavefronts' worth of CUs).  With blockIdx streams
+// (round 5) a stream whose workgroups were not resident -- another kernel holding
+// their CUs, e.g. a second process's persistent encoder on the same GPU -- left
+// every resident wave spinning in the look-back until the spin limit
+// (DESIGN.md §2 "Ticket streams and progress").  FEDCODEC_TICKET_BLOCKIDX=1 restores
+// that mapping for the regression test only.
+__device__ __forceinline__ uint32_t ticket_stream(uint32_t* started, uint32_t b, uint32_t w, uint32_t wpg,
+                                                  uint32_t nshards, uint32_t by_block, int lane) {
+  uint32_t r = 0;
+  if (lane == 0) r = atomicAdd(started, 1u);
+  r = __builtin_amdgcn_readfirstlane(r);
+  return (by_block ? b * wpg + w : r) % nshards;
 }
 #ifndef FC_STORE_ALIGN
 #define FC_STORE_ALIGN 1
@@ -289,7 +294,12 @@ __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
 __device__ __forceinline__ void st_agent2(uint64_t* p, uint64_t g0, uint64_t g1) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 v = {(uint32_t)g0, (uint32_t)(g0 >> 32), (uint32_t)g1, (uint32_t)(g1 >> 32)};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  // `s_nop 1` inside the statement: a store of more than 8 bytes reads its data
+  // VGPRs after issue, and the compiler does not see the store to pad the VALU
+  // write that may follow (gfx9 hazard; without it a status could go out with
+  // half-overwritten words -- the round-5 / round-6 illegal-address faults, DESIGN
+  // §2 "Ticket streams and progress")
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
@@ -318,8 +328,10 @@ struct EncodeArgs {
   uint64_t* status;   // [nclients * T][2]
   uint32_t* counter;  // kTicketShards ticket counters, 64 B apart (zeroed per launch)
   uint32_t nshards;   // ticket streams in use: min(kTicketShards, grid)
-  uint32_t xcd_shard; // streams by XCD group (host-checked: every stream has waves)
+  uint32_t by_block;  // regression-test knob: streams by blockIdx (round 5) instead of start order
+  uint32_t* started;  // waves started (start order -> ticket stream)
   uint32_t* spin_err;
+  uint32_t spin_limit;  // look-back polls before the safety net (default 2^24)
   const void* cparams;   // ClientParam[nclients] (workspace)
   uint32_t* slow_count;  // clients handed to the exact kernel
   int32_t* slow_flag;    // [nclients] (zeroed per launch)
@@ -349,11 +361,23 @@ __device__ __forceinline__ uint64_t quarter_rel(uint32_t off, int32_t prev, int3
 // opaque asm makes every use a fresh scalar load, so fields needed only on rare
 // paths (slow tiles, overflow, spin errors, a client's last tile) do not hold
 // SGPRs for the whole persistent loop.
+// (Kernels only: LLVM lowers __builtin_amdgcn_kernarg_segment_ptr() to NULL in any
+// function that is not a kernel, so an out-of-line callee -- lookback_deep,
+// lookback_vec_wait -- that read the arguments this way dereferenced address 0:
+// the round-5 fault in its spin-timeout branch, and round 6's first build on every
+// poll.  The look-backs take their spin limit and error word as SpinCtl instead;
+// tests/test_kernarg_use.py checks the compiled IR.)
 __device__ __forceinline__ const EncodeArgs& enc_args_fresh() {
   const EncodeArgs* p = (const EncodeArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(p));
   return *p;
 }
+
+// The look-back's safety net, passed down from the kernel's own arguments.
+struct SpinCtl {
+  uint32_t limit;  // polls before a look-back gives up (the client then goes to the exact path)
+  uint32_t* err;   // OR'ed with 1 when one did
+};
 
 __device__ __forceinline__ uint32_t div_clients(const EncodeArgs& a, uint32_t n) {
   if (a.div_l == 0) return n;  // nclients == 1
@@ -466,7 +490,7 @@ __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgc
 // pre1/pre2 (optional): this lane's status of tile t-1-lane, loaded earlier.
 template <int SPAN = kTE>  // elements per status slot (tile, or super-tile)
 __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int lane,
-                                        bool& slow, bool have_pre = false,
+                                        bool& slow, SpinCtl sc, bool have_pre = false,
                                         uint64_t pre1 = 0, uint64_t pre2 = 0) {
   Seg S = seg_identity();
   int64_t base = (int64_t)t - 1;
@@ -493,11 +517,11 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
       const uint64_t need = k >= 63 ? ~0ull : ((2ull << k) - 1);
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {  // safety net only: tickets guarantee progress
+      if (++spins > sc.limit) {  // safety net only: tickets guarantee progress
         // (a timed-out look-back's fold is not a prefix: `slow` makes the caller re-encode the
         // client -- k_encode_exact's callers through the overflow flag; the fold itself runs on,
         // which keeps this cold path from changing the encoders' register allocation)
-        if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
+        if (lane == 0) atomicOr(sc.err, 1u);
         slow = true;
         k = 0;
         w1 = kFlagPre;
@@ -545,7 +569,7 @@ __device__ unsigned long long g_stamps[16];
 constexpr uint32_t kSegSlow = 0xFFFFFFFFu;  // lookback_deep's "a slow tile" result (has_nz)
 template <int SPAN = kTE>
 __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, int lane,
-                                          uint64_t pre1, uint64_t pre2) {
+                                          uint64_t pre1, uint64_t pre2, SpinCtl sc) {
   // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
   // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
   Seg S = seg_identity();  // fold of the newer windows already walked
@@ -567,8 +591,8 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
       const uint64_t need = pre ? ~0ull << (63 - (int)__clzll(pre)) : ~0ull;
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {  // (safety net) the client goes to the exact path
-        if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
+      if (++spins > sc.limit) {  // (safety net) the client goes to the exact path
+        if (lane == 0) atomicOr(sc.err, 1u);
         Seg r = seg_identity();
         r.has_nz = kSegSlow;
         return r;
@@ -620,7 +644,7 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
     const uint32_t csum = (uint32_t)wave_sum_i((int32_t)contrib);
     if (__builtin_amdgcn_readlane(l1, 63) < 32u) {  // short newest body: exact scalar fold
       bool slow = false;
-      Seg r2 = lookback<SPAN>(status_c, t, lane, slow);
+      Seg r2 = lookback<SPAN>(status_c, t, lane, slow, sc);
       if (slow) r2.has_nz = kSegSlow;
       return r2;
     }
@@ -660,11 +684,11 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
 // scalar lookback() does the fold.  No prefix within 64 tiles: lookback_deep().
 template <int SPAN>
 __device__ __noinline__ Seg lookback_vec_wait(const uint64_t* status_c, int32_t t, int lane, uint64_t pre1,
-                                              uint64_t pre2);
+                                              uint64_t pre2, SpinCtl sc);
 template <bool WAIT, int SPAN>
 __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32_t t, int lane,
                                                  bool& slow, uint64_t pre1,
-                                                 uint64_t pre2) {
+                                                 uint64_t pre2, SpinCtl sc) {
   // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
   // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
   const int32_t ti = t - 64 + lane;
@@ -684,7 +708,7 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     p = pre ? 63 - (int)__clzll(pre) : 0;
     const uint64_t need = ~0ull << p;
     if (pre == 0 || (val & need) != need) {
-      Seg r = lookback_vec_wait<SPAN>(status_c, t, lane, pre1, pre2);
+      Seg r = lookback_vec_wait<SPAN>(status_c, t, lane, pre1, pre2, sc);
       if (r.has_nz == kSegSlow) {
         slow = true;
         r = seg_identity();
@@ -698,7 +722,7 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     const uint64_t val = __ballot(valid);
     if (pre == 0) {  // no prefix in the window: walk 64-tile windows
       FC_COUNT(10, 1);
-      Seg r = lookback_deep<SPAN>(status_c, t, lane, pre1, pre2);
+      Seg r = lookback_deep<SPAN>(status_c, t, lane, pre1, pre2, sc);
       if (r.has_nz == kSegSlow) {
         slow = true;
         r = seg_identity();
@@ -710,8 +734,8 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     if ((val & need) == need) break;
     FC_COUNT(9, 1);
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1u << 24)) {  // (safety net) the client goes to the exact path
-      if (lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
+    if (++spins > sc.limit) {  // (safety net) the client goes to the exact path
+      if (lane == 0) atomicOr(sc.err, 1u);
       slow = true;
       return seg_identity();
     }
@@ -783,16 +807,16 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
 // The waiting variant, out of line (a re-poll, or no prefix in the window).
 template <int SPAN>
 __device__ __noinline__ Seg lookback_vec_wait(const uint64_t* status_c, int32_t t, int lane, uint64_t pre1,
-                                              uint64_t pre2) {
+                                              uint64_t pre2, SpinCtl sc) {
   bool slow = false;
-  Seg r = lookback_vec_impl<true, SPAN>(status_c, t, lane, slow, pre1, pre2);
+  Seg r = lookback_vec_impl<true, SPAN>(status_c, t, lane, slow, pre1, pre2, sc);
   if (slow) r.has_nz = kSegSlow;
   return r;
 }
 template <int SPAN = kTE>
 __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t, int lane, bool& slow,
-                                            uint64_t pre1, uint64_t pre2) {
-  return lookback_vec_impl<false, SPAN>(status_c, t, lane, slow, pre1, pre2);
+                                            uint64_t pre1, uint64_t pre2, SpinCtl sc) {
+  return lookback_vec_impl<false, SPAN>(status_c, t, lane, slow, pre1, pre2, sc);
 }
 
 // Runtime-indexed read of a small register array without scratch (select chain).
@@ -1730,17 +1754,31 @@ __device__ __forceinline__ bool stage_tile(const EncodeArgs& a, ConstParamPtr cp
 __device__ __forceinline__ int stage_pos(int lane, int j) {
   return 256 * (lane >> 4) + 64 * j + 4 * ((lane + 4 * j) & 15);
 }
-// The staging reads are inline asm (their completion is waited for explicitly):
-// the compiler's wait-count pass treats any ds_read of a buffer an LDS-DMA
-// wrote as waiting on that DMA, and would otherwise drain vmcnt -- including
-// the next tile's DMA and the pending tile's stores -- at every tile start.
+// The staging reads are inline asm: the compiler's wait-count pass treats any
+// ds_read of a buffer an LDS-DMA wrote as waiting on that DMA, and would otherwise
+// drain vmcnt -- including the next tile's DMA and the pending tile's stores -- at
+// every tile start.  The four reads and their lgkmcnt wait are ONE statement with
+// early-clobber outputs: the compiler sees the registers written only once the
+// data has landed, so it cannot copy, spill or reuse them before.
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 stage_read(const uint32_t* stg, int lane, int j) {
+__device__ __forceinline__ void stage_read4(const uint32_t* stg, int lane, uint32_t (&raw)[kChunks][4]) {
+  static_assert(kChunks == 4, "four staging reads per lane");
   typedef const __attribute__((address_space(3))) uint32_t* lds_cptr;
-  const lds_cptr p = (lds_cptr)(stg + stage_pos(lane, j));
-  u32x4_t v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(p) : "memory");
-  return make_uint4(v.x, v.y, v.z, v.w);
+  u32x4_t v0, v1, v2, v3;
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %5\n\t"
+      "ds_read_b128 %2, %6\n\t"
+      "ds_read_b128 %3, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+      : "v"((lds_cptr)(stg + stage_pos(lane, 0))), "v"((lds_cptr)(stg + stage_pos(lane, 1))),
+        "v"((lds_cptr)(stg + stage_pos(lane, 2))), "v"((lds_cptr)(stg + stage_pos(lane, 3)))
+      : "memory");
+  raw[0][0] = v0.x; raw[0][1] = v0.y; raw[0][2] = v0.z; raw[0][3] = v0.w;
+  raw[1][0] = v1.x; raw[1][1] = v1.y; raw[1][2] = v1.z; raw[1][3] = v1.w;
+  raw[2][0] = v2.x; raw[2][1] = v2.y; raw[2][2] = v2.z; raw[2][3] = v2.w;
+  raw[3][0] = v3.x; raw[3][1] = v3.y; raw[3][2] = v3.z; raw[3][3] = v3.w;
 }
 
 // One wavefront = one workgroup = one 1024-element tile at a time: no barriers,
@@ -1766,7 +1804,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
   for (int i = lane; i < 2 * (kWinWords + 3); i += kEncThreads) (&wins[0][0])[i] = 0;
-  const uint32_t shard = ticket_shard(blockIdx.x, 0, 1, a.nshards, a.xcd_shard);
+  const uint32_t shard = ticket_stream(a.started, blockIdx.x, 0, 1, a.nshards, a.by_block, lane);
   uint32_t* my_counter = a.counter + kShardStride * shard;
   // Tickets run two ahead: the tile after the current one is known when the
   // current one starts, so its values are staged into LDS (LDS-DMA) while the
@@ -1845,12 +1883,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
             *(uint4*)(stg + stage_pos(lane, j)) = v;
           }
         }
-#pragma unroll
-        for (int j = 0; j < kChunks; ++j) {
-          const uint4 v = stage_read(stg, lane, j);
-          raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stage_read4(stg, lane, raw);
       }
       // the staging is free once read: stage the next tile (waited for after part C)
       staged = ticket1 < total_tiles && stage_tile(a, cparams, ticket1, stg, lane);
@@ -2031,7 +2064,7 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         excl.has_nz = 1;
         excl.first = excl.last = -1;
       } else {
-        excl = lookback_vec(a.status + 2 * (int64_t)pc * a.T, pt, lane, slow, pw1, pw2);
+        excl = lookback_vec(a.status + 2 * (int64_t)pc * a.T, pt, lane, slow, pw1, pw2, SpinCtl{a.spin_limit, a.spin_err});
         if (FC_ABL & 4096) {  // diagnostics: the look-back runs, its result is dropped
           asm volatile("" :: "s"((uint32_t)excl.body), "s"(excl.last), "s"(excl.tail));
           excl = seg_identity();
@@ -2234,7 +2267,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
   const uint32_t total = (uint32_t)a.nclients * (uint32_t)a.T2;
   const ConstParamPtr cparams = (ConstParamPtr)a.cparams;
   const int64_t P = a.P;
-  const uint32_t shard = ticket_shard(blockIdx.x, (uint32_t)wave, kEnc2Waves, a.nshards, a.xcd_shard);
+  const uint32_t shard = ticket_stream(a.started, blockIdx.x, (uint32_t)wave, kEnc2Waves, a.nshards, a.by_block, lane);
   uint32_t* my_counter = a.counter + kShardStride * shard;
   // tickets run one ahead: the next super-tile's first tile is staged while the
   // current one's second tile computes
@@ -2305,12 +2338,7 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           *(uint4*)(stg + stage_pos(lane, j)) = v;
         }
       }
-#pragma unroll
-      for (int j = 0; j < kChunks; ++j) {
-        const uint4 v = stage_read(stg, lane, j);
-        raw[j][0] = v.x; raw[j][1] = v.y; raw[j][2] = v.z; raw[j][3] = v.w;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stage_read4(stg, lane, raw);
       if (FC_ABL & 64) {  // diagnostics: synthetic values in [-2, 2), no input loads
 #pragma unroll
         for (int j = 0; j < kChunks; ++j)
@@ -2537,7 +2565,8 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           st_agent2(st, agg_word(fr, lr, body), kFlagAgg | agg_tail);
         }
         STAMP(5);
-        excl = lookback_vec<STE>(status_f + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2);
+        excl = lookback_vec<STE>(status_f + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2,
+                                 SpinCtl{a.spin_limit, a.spin_err});
         STAMP(6);
       }
     }
@@ -2624,9 +2653,12 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
 }
 
 // Reset the look-back status (and overflow flag) of the clients k_encode
-// handed over, so k_encode_exact can chain them afresh.
+// handed over, so k_encode_exact can chain them afresh.  A launch whose look-back
+// hit the spin limit (spin_err) marks those clients FC_OVERFLOW_STALL: their codes
+// are re-encoded exactly and valid, and the host reports the stall.
 __global__ void k_zero_slow(EncodeArgs a) {
   const uint32_t n = *a.slow_count;
+  const int32_t mark = *a.spin_err ? FC_OVERFLOW_STALL : 0;
   const int64_t per = 2 * (int64_t)a.T;
   const int64_t total = (int64_t)n * per;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -2634,7 +2666,7 @@ __global__ void k_zero_slow(EncodeArgs a) {
     const int64_t l = i / per;
     const int32_t c = a.slow_list[l];
     a.status[(int64_t)c * per + (i - l * per)] = 0;
-    if (i - l * per == 0) a.overflow[c] = 0;
+    if (i - l * per == 0) a.overflow[c] = mark;
   }
 }
 
@@ -2703,10 +2735,13 @@ __global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
         st_agent2(st, agg_word(fr, lr, (uint32_t)body), kFlagAgg | agg.tail);
       }
       bool slow = false;
-      excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, slow);
+      // (one global ticket counter: progress is unconditional here, so the test knob
+      // FEDCODEC_SPIN_LIMIT does not apply; the limit stays a safety net)
+      excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, slow, SpinCtl{1u << 24, a.spin_err});
       // (only a timed-out look-back: every status here is the exact kernel's own) the
       // client's code is unusable; its overflow flag makes the checked caller re-encode it
-      if (slow && lane == 0) atomicOr((uint32_t*)&enc_args_fresh().overflow[c], 1u);
+      if (slow && lane == 0)
+        atomicOr((uint32_t*)&enc_args_fresh().overflow[c], (uint32_t)(FC_OVERFLOW_CAPACITY | FC_OVERFLOW_STALL));
     }
     const Seg incl = seg_combine(excl, agg);
     SlowEmit e;
@@ -4320,106 +4355,119 @@ __device__ __forceinline__ f4row_t ld_row4(const __attribute__((address_space(1)
   if (FC_ROW_NT) return __builtin_nontemporal_load(p);
   return *p;
 }
-// Client split (few clients per GPU): client c's tiles are cut into gridDim.x
-// parts, part s = [s ntile / S, (s + 1) ntile / S), one workgroup each, so a
-// GPU's share of 64-128 clients still fills every CU.  Each part writes its
-// float64 sum and max to part[c][s]; k_norms_finalize adds the parts in order
-// (S = 1: the one-workgroup-per-client sums exactly).
-__device__ __forceinline__ void part_range(int64_t ntile, int s, int S, int64_t& lo, int64_t& hi) {
-  lo = ntile * s / S;
-  hi = ntile * (s + 1) / S;
+// Client split (few clients per GPU): a client's row is summed in REDUCTION BLOCKS
+// of kRedTiles 2048-element tiles, and each block's float64 partial is formed in an
+// order fixed by the block alone (wave w takes tiles w, w + waves, ... of the block;
+// lanes by a shuffle tree, then waves in order).  The part count S (gridDim.x:
+// workgroups per client, chosen for occupancy) only decides which workgroup forms
+// which blocks -- part s takes blocks [s nblk / S, (s + 1) nblk / S) -- and the
+// finalize kernels add a client's blocks in block order, so every sum (norms,
+// one-bit / DRIVE means, distortion) depends on P alone: the same bits for any
+// client count per GPU (tests/test_gpu_aggregators.py::
+// test_client_split_is_deterministic).
+constexpr int kRedTiles = 64;
+__host__ __device__ __forceinline__ int64_t red_blocks(int64_t P) { return ((P + 2047) / 2048 + kRedTiles - 1) / kRedTiles; }
+__device__ __forceinline__ void part_range(int64_t n, int s, int S, int64_t& lo, int64_t& hi) {
+  lo = n * s / S;
+  hi = n * (s + 1) / S;
 }
 // ACC: 0 sum |x|, 1 sum x^2, 2 none (max only).  max |x| is always taken.
 template <int ACC, bool PRE>
 __global__ __launch_bounds__(kNormThreads) void k_client_norms(const float* const* xs, int64_t P,
                                                                const float* prescale, double* part) {
-  __shared__ double red[kNormThreads / 64];
-  __shared__ float redm[kNormThreads / 64];
   const int c = blockIdx.y;
   const float* __restrict__ x = xs[c];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const float s0 = PRE ? prescale[2 * c] : 1.0f, s1 = PRE ? prescale[2 * c + 1] : 1.0f;
   const bool aligned = ((uintptr_t)x & 15u) == 0;
-  int64_t tlo, ntile;
-  part_range((P + 2047) / 2048, (int)blockIdx.x, (int)gridDim.x, tlo, ntile);
-  // one float64 accumulator per float4 component: independent chains, summed in a
-  // fixed order
-  double acc4[4] = {0.0, 0.0, 0.0, 0.0};
-  float mx = 0.0f;
+  const int64_t ntile = (P + 2047) / 2048, nblk = red_blocks(P);
+  int64_t blo, bhi;
+  part_range(nblk, (int)blockIdx.x, (int)gridDim.x, blo, bhi);
   // global (not flat) loads of the client's row
   typedef float f4v __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) float* gfptr;
   typedef const __attribute__((address_space(1))) f4v* gf4ptr;
   const gfptr xg = (gfptr)x;
-  for (int64_t tile = tlo + wv; tile < ntile; tile += kNormThreads / 64) {
-    const int64_t base = tile * 2048;
-    const bool full = base + 2048 <= P && aligned;
-    f4v raw[8];
-    if (full) {
+  for (int64_t b = blo; b < bhi; ++b) {
+    // one float64 accumulator per float4 component: independent chains, summed in a
+    // fixed order
+    double acc4[4] = {0.0, 0.0, 0.0, 0.0};
+    float mx = 0.0f;
+    const int64_t te = min(ntile, (b + 1) * kRedTiles);
+    for (int64_t tile = b * kRedTiles + wv; tile < te; tile += kNormThreads / 64) {
+      const int64_t base = tile * 2048;
+      const bool full = base + 2048 <= P && aligned;
+      f4v raw[8];
+      if (full) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) raw[k] = ld_row4((gf4ptr)(xg + base + 256 * k + 4 * lane));
-    } else {
+        for (int k = 0; k < 8; ++k) raw[k] = ld_row4((gf4ptr)(xg + base + 256 * k + 4 * lane));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int64_t e = base + 256 * k + 4 * lane;
+          raw[k].x = e < P ? xg[e] : 0.0f;
+          raw[k].y = e + 1 < P ? xg[e + 1] : 0.0f;
+          raw[k].z = e + 2 < P ? xg[e + 2] : 0.0f;
+          raw[k].w = e + 3 < P ? xg[e + 3] : 0.0f;
+        }
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const int64_t e = base + 256 * k + 4 * lane;
-        raw[k].x = e < P ? xg[e] : 0.0f;
-        raw[k].y = e + 1 < P ? xg[e + 1] : 0.0f;
-        raw[k].z = e + 2 < P ? xg[e + 2] : 0.0f;
-        raw[k].w = e + 3 < P ? xg[e + 3] : 0.0f;
+        const float v4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = v4[i] + 0.0f;  // DAZ as TF-CPU (zero padding past P adds nothing)
+          if (PRE) v = (v * s0) * s1;
+          const float a = fabsf(v);
+          mx = fmaxf(mx, a);
+          const double ad = (double)a;
+          if (ACC == 0) acc4[i] += ad;
+          if (ACC == 1) acc4[i] = fma(ad, ad, acc4[i]);
+        }
       }
     }
+    double r = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+    float m = mx;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float v4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float v = v4[i] + 0.0f;  // DAZ as TF-CPU (zero padding past P adds nothing)
-        if (PRE) v = (v * s0) * s1;
-        const float a = fabsf(v);
-        mx = fmaxf(mx, a);
-        const double ad = (double)a;
-        if (ACC == 0) acc4[i] += ad;
-        if (ACC == 1) acc4[i] = fma(ad, ad, acc4[i]);
-      }
+    for (int o = 32; o > 0; o >>= 1) {
+      r += shfl_xor_f64(r, o);
+      m = fmaxf(m, __shfl_xor(m, o));
     }
-  }
-  double r = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
-  float m = mx;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    r += shfl_xor_f64(r, o);
-    m = fmaxf(m, __shfl_xor(m, o));
-  }
-  if (lane == 0) {
-    red[wv] = r;
-    redm[wv] = m;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = red[0];
-    float tm = redm[0];
-    for (int w = 1; w < kNormThreads / 64; ++w) {
-      t += red[w];
-      tm = fmaxf(tm, redm[w]);
+    if (lane == 0) {  // (block, wave) partial: no workgroup barrier in the loop
+      double* pp = part + 2 * (((int64_t)c * nblk + b) * (kNormThreads / 64) + wv);
+      pp[0] = r;
+      pp[1] = (double)m;
     }
-    double* pp = part + 2 * ((int64_t)c * gridDim.x + blockIdx.x);
-    pp[0] = t;
-    pp[1] = (double)tm;
   }
 }
 
-// The norms from the parts of each client, added in part order (one thread per client).
-__global__ void k_norms_finalize(const double* part, int32_t nclients, int32_t nparts, int64_t P, int kind,
-                                 float* norms) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nclients) return;
-  const double* pp = part + 2 * (int64_t)c * nparts;
-  double t = pp[0];
-  float tm = (float)pp[1];
-  for (int s = 1; s < nparts; ++s) {
-    t += pp[2 * s];
-    tm = fmaxf(tm, (float)pp[2 * s + 1]);
+// The norms from each client's (block, wave) partials: one wave per client, lane l
+// adds blocks l, l + 64, ... in order (a block's waves in order), then a fixed
+// shuffle tree over the lanes -- an order set by P alone.
+__global__ __launch_bounds__(64) void k_norms_finalize(const double* part, int32_t nclients, int32_t nblk, int64_t P,
+                                                       int kind, float* norms) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  constexpr int W = kNormThreads / 64;
+  double t = 0.0;
+  float tm = 0.0f;
+  for (int64_t b = lane; b < nblk; b += 64) {
+    const double* pp = part + 2 * ((int64_t)c * nblk + b) * W;
+    double tb = pp[0];
+    float mb = (float)pp[1];
+    for (int w = 1; w < W; ++w) {
+      tb += pp[2 * w];
+      mb = fmaxf(mb, (float)pp[2 * w + 1]);
+    }
+    t += tb;
+    tm = fmaxf(tm, mb);
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    t += shfl_xor_f64(t, o);
+    tm = fmaxf(tm, __shfl_xor(tm, o));
+  }
+  if (lane != 0) return;
   float out = tm;  // FC_NORM_MAX_MAGNITUDE / FC_NORM_LINF
   if (kind == FC_NORM_MEAN_MAGNITUDE) out = (float)(t / (double)P);
   if (kind == FC_NORM_DIMENSIONLESS) out = (float)sqrt(t / (double)P);
@@ -4487,10 +4535,11 @@ __device__ __forceinline__ uint32_t dpp_row_shl(uint32_t x, int n) {
                 : __builtin_amdgcn_update_dpp(0u, x, 0x104, 0xf, 0xf, false);
 }
 
-// Client split as k_client_norms: grid (S, C), part s of client c codes tiles
-// [s ntile / S, (s + 1) ntile / S) (in the client's rotated tile order) and
-// writes its sums to part[c][s] = {S1, S2, A1, A2, count}; k_mask_finalize adds
-// the parts in order and forms the means and the distortion.
+// Client split as k_client_norms: grid (S, C), part s of client c codes reduction
+// blocks [s nblk / S, (s + 1) nblk / S) of the client's rotated block order (wave w:
+// tiles w, w + 4, ... of each block) and writes block b's sums to part[c][b] = {S1,
+// S2, A1, A2, count}; k_mask_finalize adds the blocks in block order and forms the
+// means and the distortion (sums fixed by P alone).
 constexpr int kObPart = 5;  // doubles per part
 #ifndef FC_OB_F32X
 #define FC_OB_F32X 0  // sums of x (and of x over the mask) in float32 tile partials (A/B knob; 0: float64)
@@ -4505,17 +4554,15 @@ __attribute__((amdgpu_waves_per_eu(FC_OB_WPE)))
 #endif
 void k_mask_encode(const float* const* xs, int64_t P, float thr,
                                                             uint32_t* masks, double* part) {
-  __shared__ double red[4][kObWaves];
-  __shared__ uint64_t redn[kObWaves];
   __shared__ uint32_t wordbuf[kObWaves][64];
   const int c = blockIdx.y;
   const float* __restrict__ x = xs[c];
   const int64_t nw = (P + 31) / 32;
   uint32_t* __restrict__ m = masks + (int64_t)c * nw;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t ntile = (P + 2047) / 2048;
-  int64_t tlo, thi;  // this part's tiles, in rotated order
-  part_range(ntile, (int)blockIdx.x, (int)gridDim.x, tlo, thi);
+  const int64_t ntile = (P + 2047) / 2048, nblk = red_blocks(P);
+  int64_t blo, bhi;  // this part's reduction blocks, in rotated order
+  part_range(nblk, (int)blockIdx.x, (int)gridDim.x, blo, bhi);
   const bool aligned = ((uintptr_t)x & 15u) == 0;
   // KIND 0: s1 = sum x, s2 = sum x^2, a1 / a2 = the same over x >= thr;
   // KIND 1: s1 = sum |x|, s2 = sum x^2.  Sums of x in float64 (FC_OB_F32X: float32
@@ -4529,8 +4576,17 @@ void k_mask_encode(const float* const* xs, int64_t P, float thr,
 #ifndef FC_OB_ROTATE
 #define FC_OB_ROTATE 1
 #endif
-  const int64_t t0 = FC_OB_ROTATE ? ((int64_t)c * 977) % ntile : 0;
-  auto tile_of = [&](int64_t tt) { return tt + t0 < ntile ? tt + t0 : tt + t0 - ntile; };
+  const int64_t b0 = FC_OB_ROTATE ? ((int64_t)c * 977) % nblk : 0;
+  // the wave's k-th tile of this part: block blo + k / kPerWave (rotated), tile
+  // wv + kObWaves (k mod kPerWave) of it; -1 past the client's last tile (its last
+  // block may be partial)
+  constexpr int kPerWave = kRedTiles / kObWaves;
+  auto tile_of = [&](int64_t k) -> int64_t {
+    int64_t b = blo + k / kPerWave + b0;
+    if (b >= nblk) b -= nblk;
+    const int64_t t = b * kRedTiles + wv + kObWaves * (k % kPerWave);
+    return t < ntile ? t : -1;
+  };
   // global (not flat) loads: a flat load also counts in lgkmcnt, so every LDS
   // wait of the word assembly would wait for the in-flight tile too
   typedef float f4v __attribute__((ext_vector_type(4)));
@@ -4610,81 +4666,77 @@ void k_mask_encode(const float* const* xs, int64_t P, float thr,
     const uint32_t word = wordbuf[wv][lane];
     if (tile * 64 + lane < nw) m[tile * 64 + lane] = word;
   };
-#ifndef FC_OB_PIPE
-#define FC_OB_PIPE 1  // the next tile's loads in flight while a tile computes (0: one tile per wave at a time)
-#endif
-  if (FC_OB_PIPE) {
-    // software-pipelined: the next tile's loads are in flight while a tile computes
-    f4v ra[8], rb[8];
-    if (tlo + wv < thi) load_tile(tile_of(tlo + wv), ra);
-    for (int64_t tt = tlo + wv; tt < thi; tt += 2 * kObWaves) {
-      const int64_t tn = tt + kObWaves;
-      if (tn < thi) load_tile(tile_of(tn), rb);
-      do_tile(tile_of(tt), ra);
-      if (tn >= thi) break;
-      if (tn + kObWaves < thi) load_tile(tile_of(tn + kObWaves), ra);
-      do_tile(tile_of(tn), rb);
+  // a block's sums of this wave, lanes reduced by a fixed shuffle tree, to its
+  // (block, wave) slot: no workgroup barrier in the loop (k_mask_finalize adds the
+  // waves and blocks in a fixed order)
+  auto flush = [&](int64_t k) {
+    const double S1w = wave_sum_f64(s1), S2w = wave_sum_f64(s2), A1w = wave_sum_f64(a1), A2w = wave_sum_f64(a2);
+    const uint32_t nsum = (uint32_t)wave_sum_i((int32_t)na);
+    s1 = s2 = a1 = a2 = 0.0;
+    na = 0;
+    if (lane == 0) {
+      int64_t b = blo + k / kPerWave + b0;
+      if (b >= nblk) b -= nblk;
+      double* pp = part + kObPart * (((int64_t)c * nblk + b) * kObWaves + wv);
+      pp[0] = S1w;
+      pp[1] = S2w;
+      pp[2] = A1w;
+      pp[3] = A2w;
+      pp[4] = (double)nsum;
     }
-  } else {
-    // one tile per wave at a time, fewer registers: more waves keep more bytes in flight
-    for (int64_t tt = tlo + wv; tt < thi; tt += kObWaves) {
-      f4v ra[8];
-      load_tile(tile_of(tt), ra);
-      do_tile(tile_of(tt), ra);
-    }
-  }
-  // fixed-order reductions: lanes (shuffle tree), then waves in order
-  s1 = wave_sum_f64(s1);
-  s2 = wave_sum_f64(s2);
-  a1 = wave_sum_f64(a1);
-  a2 = wave_sum_f64(a2);
-  const uint32_t nsum = (uint32_t)wave_sum_i((int32_t)na);
-  if (lane == 0) {
-    red[0][wv] = s1;
-    red[1][wv] = s2;
-    red[2][wv] = a1;
-    red[3][wv] = a2;
-    redn[wv] = nsum;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double S1 = 0.0, S2 = 0.0, A1 = 0.0, A2 = 0.0;
-    uint64_t n_ = 0;
-    for (int w = 0; w < kObWaves; ++w) {
-      S1 += red[0][w];
-      S2 += red[1][w];
-      A1 += red[2][w];
-      A2 += red[3][w];
-      n_ += redn[w];
-    }
-    double* pp = part + kObPart * ((int64_t)c * gridDim.x + blockIdx.x);
-    pp[0] = S1;
-    pp[1] = S2;
-    pp[2] = A1;
-    pp[3] = A2;
-    pp[4] = (double)n_;
+  };
+  // software-pipelined: the wave's next tile's loads are in flight while a tile
+  // computes (across block ends too); every wave walks kPerWave slots per block, so
+  // all reach each block's reduction together
+  const int64_t K = kPerWave * (bhi - blo);
+  f4v ra[8], rb[8];
+  int64_t ta = K > 0 ? tile_of(0) : -1;
+  if (ta >= 0) load_tile(ta, ra);
+  for (int64_t k = 0; k < K; k += 2) {  // K is even (kPerWave is)
+    const int64_t tb = tile_of(k + 1);
+    if (tb >= 0) load_tile(tb, rb);
+    if (ta >= 0) do_tile(ta, ra);
+    ta = k + 2 < K ? tile_of(k + 2) : -1;
+    if (ta >= 0) load_tile(ta, ra);
+    if (tb >= 0) do_tile(tb, rb);
+    if ((k + 2) % kPerWave == 0) flush(k);
   }
 }
 
-// Means and distortion of each client from its parts, added in part order (one
-// thread per client).
+// Means and distortion of each client from its (block, wave) partials: one wave
+// per client, lane l adds blocks l, l + 64, ... in order (a block's waves in
+// order), then a fixed shuffle tree -- an order set by P alone.
 template <int KIND>
-__global__ void k_mask_finalize(const double* part, int32_t nclients, int32_t nparts, int64_t P,
-                                int min_distortion, float* means, double* dist) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nclients) return;
-  {
-    const double* pp = part + kObPart * (int64_t)c * nparts;
-    double S1 = pp[0], S2 = pp[1], A1 = pp[2], A2 = pp[3];
-    uint64_t n_ = (uint64_t)pp[4];
-    for (int s = 1; s < nparts; ++s) {
-      const double* q = pp + kObPart * s;
-      S1 += q[0];
-      S2 += q[1];
-      A1 += q[2];
-      A2 += q[3];
+__global__ __launch_bounds__(64) void k_mask_finalize(const double* part, int32_t nclients, int32_t nblk, int64_t P,
+                                                      int min_distortion, float* means, double* dist) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  double S1 = 0.0, S2 = 0.0, A1 = 0.0, A2 = 0.0;
+  uint64_t n_ = 0;
+  for (int64_t b = lane; b < nblk; b += 64) {
+    const double* pp = part + kObPart * ((int64_t)c * nblk + b) * kObWaves;
+    double b1 = pp[0], b2 = pp[1], c1 = pp[2], c2 = pp[3];
+    n_ += (uint64_t)pp[4];
+    for (int w = 1; w < kObWaves; ++w) {
+      const double* q = pp + kObPart * w;
+      b1 += q[0];
+      b2 += q[1];
+      c1 += q[2];
+      c2 += q[3];
       n_ += (uint64_t)q[4];
     }
+    S1 += b1;
+    S2 += b2;
+    A1 += c1;
+    A2 += c2;
+  }
+  S1 = wave_sum_f64(S1);
+  S2 = wave_sum_f64(S2);
+  A1 = wave_sum_f64(A1);
+  A2 = wave_sum_f64(A2);
+  n_ = (uint64_t)wave_sum_i((int32_t)n_);
+  if (lane != 0) return;
+  {
     float mb, ma;
     double d_;
     if (KIND == 0) {
@@ -5062,6 +5114,23 @@ __global__ __launch_bounds__(256) void k_copy_f4(uint4* __restrict__ dst_, const
   for (; i < n; i += 256) dst[i] = src[i];
 }
 
+// Test utility (tests/test_gpu_progress.py): a workgroup holding a whole CU (all
+// 160 KiB of LDS) for `ticks` of the 100 MHz real-time clock when its XCD's bit is
+// set in xcd_mask (HW_REG_XCC_ID; the others exit at once) -- another kernel then
+// cannot place a workgroup on the masked XCDs until it ends.  Bounded: every wave
+// leaves after `ticks`.  `held` (nullable) counts the workgroups that held a CU.
+__global__ __launch_bounds__(64) void k_occupy(uint32_t xcd_mask, uint64_t ticks, int32_t* held) {
+  __shared__ uint32_t pin[40960];  // 160 KiB: one workgroup per CU
+  uint32_t xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  if (!((xcd_mask >> (xcc & 7u)) & 1u)) return;
+  pin[threadIdx.x] = threadIdx.x;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+  __syncthreads();
+  if (threadIdx.x == 0 && held && pin[63] == 63u) atomicAdd(held, 1);
+}
+
 // Rademacher sign flip (the DFT rotation's D, the same stream as k_fwht_pass's):
 // rows[c][i] *= sign of bit 31 of Philox output word i % 4 of counter i / 4.
 __global__ __launch_bounds__(256) void k_sign_flip(float* const* rows, int64_t n, Key4 key) {
@@ -5344,15 +5413,23 @@ int64_t tiles_for(int64_t P) { return (P + kTE - 1) / kTE; }
 
 // Library-owned device scratch for small per-launch partials (the client-split
 // reductions), one grow-only buffer per (device, stream): calls on one stream run
-// in order, so a stream's buffer is never used by two launches at once.
-void* scratch_for(hipStream_t s, size_t bytes) {
+// in order, so a stream's buffer is never used by two launches at once.  Growing
+// it allocates (and frees the old buffer after a sync of the stream), which a
+// stream under graph capture does not allow: there the call fails unless the buffer
+// is already large enough (warm it with one uncaptured call of the same size).
+int scratch_for(hipStream_t s, size_t bytes, void** out) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> bufs;
+  *out = nullptr;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(-10, "scratch: hipGetDevice");
   std::lock_guard<std::mutex> g(mu);
   std::pair<void*, size_t>& b = bufs[std::make_pair(dev, s)];
   if (b.second < bytes) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+      return fail(-1, "client-split scratch must grow, which is not possible while the stream is captured: "
+                      "run the call once uncaptured first");
     if (b.first) {
       (void)hipStreamSynchronize(s);  // the old buffer may still be read by this stream's last launch
       (void)hipFree(b.first);
@@ -5362,11 +5439,12 @@ void* scratch_for(hipStream_t s, size_t bytes) {
     const size_t want = std::max<size_t>(bytes, 64 << 10);
     if (hipMalloc(&b.first, want) != hipSuccess) {
       b.first = nullptr;
-      return nullptr;
+      return fail(-3, "scratch allocation failed");
     }
     b.second = want;
   }
-  return b.first;
+  *out = b.first;
+  return 0;
 }
 
 // Workgroups per client for the per-client streaming passes (k_client_norms,
@@ -5388,24 +5466,26 @@ int launch_mask_encode(const float* const* xs, int32_t nclients, int64_t P, floa
   // four times the co-resident workgroups (parts per client): the last ones finish
   // together instead of one long row each (1024 x 25 M -4.5 %, 128 clients -7 %,
   // profiles/r05/diag_parts_mult.txt)
+  const int64_t nblk = red_blocks(P);
   int parts = client_parts(nclients, (P + 2047) / 2048, 16);
-  if (const char* e = getenv("FEDCODEC_OB_PARTS"))  // test knob
-    parts = (int)std::max<int64_t>(1, std::min<int64_t>(atoi(e), (P + 2047) / 2048));
-  double* part = (double*)scratch_for(s, sizeof(double) * kObPart * (size_t)nclients * parts);
-  if (!part) return fail(-3, "scratch allocation failed");
+  if (const char* e = getenv("FEDCODEC_OB_PARTS")) parts = std::max(1, atoi(e));  // test knob
+  parts = (int)std::min<int64_t>(parts, nblk);
+  double* part = nullptr;
+  if (const int rc = scratch_for(s, sizeof(double) * kObPart * kObWaves * (size_t)nclients * nblk, (void**)&part))
+    return rc;
   hipLaunchKernelGGL(k_mask_encode<KIND>, dim3((unsigned)parts, (unsigned)nclients), dim3(kObThreads), 0, s, xs, P,
                      thr, masks, part);
   if (const int rc = check_launch("k_mask_encode")) return rc;
-  hipLaunchKernelGGL(k_mask_finalize<KIND>, dim3((nclients + 255) / 256), dim3(256), 0, s, (const double*)part,
-                     nclients, parts, P, min_distortion, means, dist);
+  hipLaunchKernelGGL(k_mask_finalize<KIND>, dim3((unsigned)nclients), dim3(64), 0, s, (const double*)part,
+                     nclients, (int32_t)nblk, P, min_distortion, means, dist);
   return check_launch("k_mask_finalize");
 }
 
 
 // Workspace: [status n*T*16][header: ticket shards, spin_err, counter2,
-// slow_count][slow_flag n*4] (all zeroed per launch) [slow_list n*4]
+// slow_count, started][slow_flag n*4] (all zeroed per launch) [slow_list n*4]
 // [ClientParam n*64].
-constexpr int kHdrWords = kShardStride * (kTicketShards + 3);
+constexpr int kHdrWords = kShardStride * (kTicketShards + 4);
 int64_t enc_status_bytes(int32_t n, int64_t P) { return (int64_t)n * tiles_for(P) * 16; }
 int64_t enc_zeroed_bytes(int32_t n, int64_t P) {
   return enc_status_bytes(n, P) + 4 * kHdrWords + 4 * (int64_t)n;
@@ -5489,7 +5569,12 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   a.spin_err = a.counter + kShardStride * kTicketShards;
   a.counter2 = a.counter + kShardStride * (kTicketShards + 1);
   a.slow_count = a.counter + kShardStride * (kTicketShards + 2);
+  a.started = a.counter + kShardStride * (kTicketShards + 3);
   a.slow_flag = (int32_t*)(a.counter + kHdrWords);
+  a.spin_limit = 1u << 24;
+  if (const char* e = getenv("FEDCODEC_SPIN_LIMIT")) a.spin_limit = (uint32_t)std::max(1L, atol(e));  // test knob
+  a.by_block = 0;
+  if (const char* e = getenv("FEDCODEC_TICKET_BLOCKIDX")) a.by_block = atoi(e) != 0;  // regression-test knob
   a.slow_list = a.slow_flag + nclients;
   a.cparams = (const uint8_t*)workspace + enc_params_offset(nclients, P);
   int dev = 0, ncu = 256;
@@ -5568,8 +5653,8 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   }
   const int wpg = super ? kEnc2Waves : 1;  // waves per workgroup
   const int64_t tickets = super ? (int64_t)nclients * a.T2 : total;
-  // Persistent grid no larger than what is co-resident (every ticket stream has a
-  // running wave); very few clients: cap the tiles in flight per client (about
+  // Persistent grid no larger than what fits co-resident on an idle chip (progress
+  // needs only kTicketShards started waves, ticket_stream); very few clients: cap the tiles in flight per client (about
   // 256) so a look-back walks at most a few 64-tile windows.
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kEncThreads * wpg, 0) != hipSuccess || per_cu < 1)
@@ -5578,12 +5663,6 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   if (const char* g = getenv("FEDCODEC_ENC_GRID")) max_grid = std::max(1L, atol(g));  // test knob
   const int grid = (int)std::min<int64_t>(tickets, max_grid);  // waves
   a.nshards = (uint32_t)std::min(kTicketShards, grid);
-  {  // XCD-group streams when each group's waves cover its nshards / 8 streams
-    const int64_t nblocks = (grid + wpg - 1) / wpg;
-    bool want = FC_XCD_SHARD;
-    if (const char* e = getenv("FEDCODEC_XCD_SHARD")) want = atoi(e) != 0;  // test knob
-    a.xcd_shard = want && a.nshards % 8 == 0 && (nblocks / 8) * wpg >= (int64_t)a.nshards / 8;
-  }
   {  // look-back prefetch window: 64 statuses when few tiles of a client are in flight,
      // 16 when many are (measured at 25 M: C = 128 -13 %, C = 1024 +2 % with 16)
     int win = kLookbackWin;
@@ -5595,12 +5674,12 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
                      (ClientParam*)a.cparams, (int)(!int_in && mode != FC_UNIFORM));
   if (hipGetLastError() != hipSuccess) return fail(-10, "k_client_params launch");
   hipLaunchKernelGGL(kern, dim3((grid + wpg - 1) / wpg), dim3(kEncThreads * wpg), 0, s, a);
-  if (hipGetLastError() != hipSuccess) return check_launch("k_encode");
+  if (const int rc_ = check_launch("k_encode")) return rc_;
   // clients with a tile beyond the fast path: exact re-encode (no-ops otherwise)
   hipLaunchKernelGGL(k_zero_slow, dim3(256), dim3(256), 0, s, a);
   hipLaunchKernelGGL(exact, dim3(grid), dim3(kEncThreads), 0, s, a);
   if (idxq) {
-    if (hipGetLastError() != hipSuccess) return check_launch("k_encode_exact");
+    if (const int rc_ = check_launch("k_encode_exact")) return rc_;
     hipLaunchKernelGGL(k_quarter_index, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, idx, idxq,
                        nclients, (int32_t)T);
     return check_launch("k_quarter_index");
@@ -5727,7 +5806,7 @@ __global__ __launch_bounds__(64) void k_seg_plan(SegArgs a) {
     last = (int64_t)(vi[Tk] >> 36) - 1;
     const int64_t nb = a.vbits[v];
     src = a.vstream + a.vstream_off[v];
-    ovf = a.vovf[v] != 0;
+    ovf = (uint32_t)a.vovf[v];
     if (last >= 0) {
       // the segment's first code is gamma(f + 1): z zeros, then z + 1 value bits
       // (its first words are stored even when the segment overflowed its staging)
@@ -5740,6 +5819,9 @@ __global__ __launch_bounds__(64) void k_seg_plan(SegArgs a) {
       const int64_t trail = last < Pk - 1 ? (int64_t)glen64((uint64_t)(Pk - last)) : 0;
       body = nb - oldR - trail;
       gl = sk + last;
+      // a segment code that contradicts its own index (it cannot happen for a code the
+      // encoder completed) is never stitched: the client is re-encoded (capacity flag)
+      if (body < 0 || f < 0 || f > last) ovf |= FC_OVERFLOW_CAPACITY;
     }
   }
   gls[k] = gl;
@@ -5753,7 +5835,8 @@ __global__ __launch_bounds__(64) void k_seg_plan(SegArgs a) {
     len = newR + body;
   }
   lens[k] = live ? len : 0;
-  const uint64_t bad = __ballot(live && ovf != 0);
+  const uint64_t bad = __ballot(live && (ovf & FC_OVERFLOW_CAPACITY) != 0);
+  const uint64_t stall = __ballot(live && (ovf & FC_OVERFLOW_STALL) != 0);
   __syncthreads();
   SegPlan* pl = a.plan + (int64_t)c * (a.nseg + 1);
   int64_t O = 0;
@@ -5792,7 +5875,8 @@ __global__ __launch_bounds__(64) void k_seg_plan(SegArgs a) {
     pl[a.nseg] = t;
     const int64_t total = sum + t.newR;
     a.total_bits[c] = total;
-    a.overflow[c] = (bad != 0 || (total + 31) / 32 * 4 > a.stream_cap[c]) ? 1 : 0;
+    a.overflow[c] = ((bad != 0 || total < 0 || (total + 31) / 32 * 4 > a.stream_cap[c]) ? FC_OVERFLOW_CAPACITY : 0) |
+                    (stall != 0 ? FC_OVERFLOW_STALL : 0);
   }
 }
 
@@ -5851,7 +5935,7 @@ __global__ __launch_bounds__(256) void k_seg_copy(SegArgs a, int64_t blocks_per_
       __syncthreads();
       const SegPlan* src_pl = a.plan + (int64_t)c * (a.nseg + 1);
       for (int i = threadIdx.x; i <= a.nseg; i += blockDim.x) pl[i] = src_pl[i];
-      if (threadIdx.x == 0) sh_total = a.overflow[c] ? 0 : src_pl[a.nseg].O + src_pl[a.nseg].len;
+      if (threadIdx.x == 0) sh_total = (a.overflow[c] & FC_OVERFLOW_CAPACITY) ? 0 : src_pl[a.nseg].O + src_pl[a.nseg].len;
       __syncthreads();
       cur = c;
     }
@@ -6276,7 +6360,7 @@ int fft_pow2(float2* b0, float2* b1, int64_t N, float sign, hipStream_t s, float
     else if (R == 8) hipLaunchKernelGGL(k_fft_pass<8>, grid, dim3(256), 0, s, src, dst, N, Ns, sign);
     else if (R == 4) hipLaunchKernelGGL(k_fft_pass<4>, grid, dim3(256), 0, s, src, dst, N, Ns, sign);
     else hipLaunchKernelGGL(k_fft_pass<2>, grid, dim3(256), 0, s, src, dst, N, Ns, sign);
-    if (hipGetLastError() != hipSuccess) return check_launch("k_fft_pass");
+    if (const int rc = check_launch("k_fft_pass")) return rc;
     Ns *= R;
     std::swap(src, dst);
   }
@@ -6591,7 +6675,7 @@ int fc_vote_lengths(const float* const* xs, int32_t nclients, int64_t P, const f
   if (mode == FC_UNIFORM) hipLaunchKernelGGL(k_vote_tiles<FC_UNIFORM>, grid, dim3(64), 0, s, a);
   else if (mode == FC_STOCHASTIC) hipLaunchKernelGGL(k_vote_tiles<FC_STOCHASTIC>, grid, dim3(64), 0, s, a);
   else hipLaunchKernelGGL(k_vote_tiles<FC_DITHERED>, grid, dim3(64), 0, s, a);
-  if (hipGetLastError() != hipSuccess) return check_launch("k_vote_tiles");
+  if (const int rc_ = check_launch("k_vote_tiles")) return rc_;
   hipLaunchKernelGGL(k_vote_finalize, dim3((unsigned)((int64_t)nclients * K)), dim3(256), 0, s, a);
   return check_launch("k_vote_finalize");
 }
@@ -6695,7 +6779,7 @@ int fc_hadamard(float* const* rows, int32_t nclients, int64_t n, int inverse, in
     const int64_t groups = (int64_t)nclients * (n / gsize);
     hipLaunchKernelGGL(k_fwht_pass, dim3((unsigned)groups), dim3(256), 0, s, rows, n, L0, k,
                        (int)(first && !inverse), (int)(last && inverse), last ? scale : 1.0f, seed0, seed1);
-    if (hipGetLastError() != hipSuccess) return check_launch("k_fwht_pass");
+    if (const int rc_ = check_launch("k_fwht_pass")) return rc_;
     if (levels == 0) break;
     L0 += k;
   }
@@ -6751,6 +6835,16 @@ int fc_copy(void* dst, const void* src, int64_t nbytes, void* stream) {
   return check_launch("k_copy_f4");
 }
 
+int fc_diag_occupy(uint32_t xcd_mask, int64_t microseconds, int32_t* held, void* stream) {
+  if (microseconds < 0 || microseconds > 5000000) return fail(-1, "fc_diag_occupy: 0 .. 5,000,000 microseconds");
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  hipLaunchKernelGGL(k_occupy, dim3((unsigned)ncu), dim3(64), 0, (hipStream_t)stream, xcd_mask & 0xFFu,
+                     (uint64_t)microseconds * 100u, held);
+  return check_launch("k_occupy");
+}
+
 int fc_dequantize(const int32_t* sum, int64_t P, float step, const float* noise_sum, float* out,
                   void* stream) {
   if (P < 0) return fail(-1, "P < 0");
@@ -6785,13 +6879,15 @@ int fc_client_norms_scaled(const float* const* xs, int32_t nclients, int64_t P, 
       prescale ? (acc == 0 ? k_client_norms<0, true> : acc == 1 ? k_client_norms<1, true> : k_client_norms<2, true>)
                : (acc == 0 ? k_client_norms<0, false> : acc == 1 ? k_client_norms<1, false> : k_client_norms<2, false>);
   hipStream_t s = (hipStream_t)stream;
-  const int parts = client_parts(nclients, (P + 2047) / 2048, 8);  // 4x the resident workgroups (-1 to -2 %)
-  double* part = (double*)scratch_for(s, sizeof(double) * 2 * (size_t)nclients * parts);
-  if (!part) return fail(-3, "scratch allocation failed");
+  const int64_t nblk = red_blocks(P);
+  const int parts = (int)std::min<int64_t>(nblk, client_parts(nclients, (P + 2047) / 2048, 8));  // 4x the resident workgroups (-1 to -2 %)
+  double* part = nullptr;
+  if (const int rc = scratch_for(s, sizeof(double) * 2 * (kNormThreads / 64) * (size_t)nclients * nblk, (void**)&part))
+    return rc;
   hipLaunchKernelGGL(kern, dim3((unsigned)parts, (unsigned)nclients), dim3(kNormThreads), 0, s, xs, P, prescale, part);
   if (const int rc = check_launch("k_client_norms")) return rc;
-  hipLaunchKernelGGL(k_norms_finalize, dim3((nclients + 255) / 256), dim3(256), 0, s, (const double*)part, nclients,
-                     parts, P, kind, norms);
+  hipLaunchKernelGGL(k_norms_finalize, dim3((unsigned)nclients), dim3(64), 0, s, (const double*)part, nclients,
+                     (int32_t)nblk, P, kind, norms);
   return check_launch("k_norms_finalize");
 }
 

@@ -84,6 +84,10 @@ extern "C" {
                                         take P <= 2^26 - 1; fc_quantize_encode_segmented cuts longer
                                         tensors into rows of at most this many elements */
 
+/* overflow[] flags of the encoders. */
+#define FC_OVERFLOW_CAPACITY 1
+#define FC_OVERFLOW_STALL 2
+
 const char* fc_last_error(void);
 const char* fc_version(void);
 
@@ -120,8 +124,12 @@ int fc_quantize(const float* x, int64_t P, float step, int64_t seed0, int64_t se
  *   total_bits  device int64[nclients]: exact code length in bits
  *   dist_part   device float[nclients * tiles]: per-tile sum (x - deq)^2
  *   nnz_part    device int32[nclients * tiles]: per-tile nonzero count
- *   overflow    device int32[nclients]: set to 1 when stream_cap[c] is too small
- *               (the code is then incomplete; total_bits is still exact)
+ *   overflow    device int32[nclients], bit flags (zeroed by the call):
+ *               FC_OVERFLOW_CAPACITY when stream_cap[c] is too small (the code is
+ *               then incomplete; total_bits is still exact); FC_OVERFLOW_STALL when
+ *               a look-back of this launch hit its spin limit and client c was
+ *               re-encoded on the exact path (the code is complete and exact; the
+ *               flag reports lost progress, DESIGN.md §2 "Ticket streams")
  * Bit-exact on q and on the bitstream vs the oracle's restatement. */
 int fc_quantize_encode(const float* const* xs, int32_t nclients, int64_t P, float step,
                        const float* norms, const float* prescale, const int64_t* seeds, int mode,
@@ -396,6 +404,14 @@ int fc_dft_rotate(float* const* rows, int32_t nclients, int64_t n, int inverse, 
  * of 16, 16-byte aligned pointers; a grid-stride 16-byte-per-lane copy whose rate
  * bench.py reports as the achievable HBM streaming peak beside the codec kernels. */
 int fc_copy(void* dst, const void* src, int64_t nbytes, void* stream);
+
+/* Test utility (not a reference interface): occupy every CU of the XCDs whose bit
+ * is set in xcd_mask (bits 0..7 = HW_REG_XCC_ID) for `microseconds` (<= 5 s) with
+ * one workgroup per CU that holds all of its LDS, so that concurrent kernels on
+ * other streams cannot use those CUs meanwhile (tests/test_gpu_progress.py: the
+ * encoder's ticket streams make progress on the remaining XCDs).  `held`
+ * (nullable device int32) is incremented once per workgroup that held a CU. */
+int fc_diag_occupy(uint32_t xcd_mask, int64_t microseconds, int32_t* held, void* stream);
 
 /* Measurement utility (not a reference interface): the encoder's arithmetic floor
  * -- read every x, draw TF's Philox4x32-10 stream, apply the exact quantiser

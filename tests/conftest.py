@@ -11,6 +11,8 @@ if ROOT not in sys.path:
 def pytest_configure(config):
   config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
   config.addinivalue_line("markers", "slow: long-running CPU test")
+  # an encoder look-back that hits its spin limit is a failure in every test
+  config.addinivalue_line("filterwarnings", "error::federated_amd.codec.EncoderStallWarning")
 
 
 @pytest.fixture(scope="session")

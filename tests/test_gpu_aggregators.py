@@ -547,3 +547,42 @@ def test_client_split_passes(gpu, C):
     np.testing.assert_allclose(dist[c], ((x - dec).astype(np.float64) ** 2).sum(), rtol=1e-6)
     scale = (xd ** 2).sum() / np.abs(xd).sum()
     np.testing.assert_allclose(dmeans[c], [-scale, scale], rtol=1e-6)
+
+
+def test_client_split_is_deterministic(gpu, monkeypatch):
+  """the client split's float64 sums are formed per reduction block of
+  64 x 2048 elements in an order fixed by P alone, so the norms, the one-bit / DRIVE
+  means and the distortion of a client are the same bits whether it is encoded with
+  1024 clients on one GPU (few parts per client) or in a 128- or 16-client share of
+  an 8-GPU round (many parts), and for any forced part count."""
+  P = (1 << 20) + 4099  # 9 reduction blocks, the last one partial
+  C = 1024
+  g = torch.Generator(device=gpu)
+  g.manual_seed(77)
+  xs = torch.randn(C, P, generator=g, device=gpu, dtype=torch.float32)
+  xs[5] += 1000.0  # a client whose one-pass distortion cancels (k_mask_distortion)
+  rows = [xs[c] for c in range(C)]
+
+  def run(sub):
+    both = codec.client_norms(sub, _lib.NORM_L2_LINF).cpu().numpy()
+    mean = codec.client_norms(sub, _lib.NORM_MEAN_MAGNITUDE).cpu().numpy()
+    rms = codec.client_norms(sub, _lib.NORM_DIMENSIONLESS).cpu().numpy()
+    masks, means, dist = codec.onebit_encode(sub, 0.0)
+    _, dmeans, ddist = codec.drive_encode(sub)
+    return (both.reshape(2, -1), mean, rms, masks.cpu().numpy().reshape(len(sub), -1),
+            means.cpu().numpy().reshape(-1, 2), dist.cpu().numpy(), dmeans.cpu().numpy().reshape(-1, 2),
+            ddist.cpu().numpy())
+
+  full = run(rows)
+  for lo, hi in ((0, 128), (128, 144), (5, 6)):
+    part = run(rows[lo:hi])
+    for a, b in zip(full, part):
+      a = a[:, lo:hi] if a.ndim == 2 and a.shape[0] == 2 and a.shape[1] == C else a[lo:hi]
+      np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
+  monkeypatch.setenv("FEDCODEC_OB_PARTS", "3")
+  forced = run(rows[:16])
+  for a, b in zip(full, forced):
+    a = a[:, :16] if a.ndim == 2 and a.shape[0] == 2 and a.shape[1] == C else a[:16]
+    np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
+  del xs, rows
+  torch.cuda.empty_cache()
