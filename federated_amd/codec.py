@@ -162,10 +162,18 @@ def index_codes(batch, nbytes, max_bytes, quarters=None, stream=None, check=True
     # run the whole rebuild on `stream`: it first waits for the work queued so far (the
     # streams' H2D copy, nbytes), and the workspace / err tensors are then allocated on
     # it, so the caching allocator cannot hand them out while the index kernels run
-    stream.wait_stream(torch.cuda.current_stream(device))
+    cur = torch.cuda.current_stream(device)
+    stream.wait_stream(cur)
     nbytes.record_stream(stream)
     with torch.cuda.stream(stream):
-      return index_codes(batch, nbytes, max_bytes, quarters=quarters, stream=None, check=check)
+      err = index_codes(batch, nbytes, max_bytes, quarters=quarters, stream=None, check=False)
+    # the rebuilt index, bit lengths and flags are read on the caller's stream next
+    # (decode, check_overflow): it waits for the rebuild
+    cur.wait_stream(stream)
+    err.record_stream(cur)
+    if check and int(err.item()):
+      raise ValueError("malformed run-length gamma code")
+    return err
   C, P = batch.nclients, batch.P
   want_q = quarter_index_wanted(C) if quarters is None else bool(quarters)
   need = int(_lib.load().fc_index_workspace_bytes(C, int(max_bytes)))

@@ -331,7 +331,6 @@ struct EncodeArgs {
   uint32_t by_block;  // regression-test knob: streams by blockIdx (round 5) instead of start order
   uint32_t* started;  // waves started (start order -> ticket stream)
   uint32_t* spin_err;
-  uint32_t spin_limit;  // look-back polls before the safety net (default 2^24)
   const void* cparams;   // ClientParam[nclients] (workspace)
   uint32_t* slow_count;  // clients handed to the exact kernel
   int32_t* slow_flag;    // [nclients] (zeroed per launch)
@@ -365,7 +364,8 @@ __device__ __forceinline__ uint64_t quarter_rel(uint32_t off, int32_t prev, int3
 // function that is not a kernel, so an out-of-line callee -- lookback_deep,
 // lookback_vec_wait -- that read the arguments this way dereferenced address 0:
 // the round-5 fault in its spin-timeout branch, and round 6's first build on every
-// poll.  The look-backs take their spin limit and error word as SpinCtl instead;
+// poll.  The out-of-line look-backs read their spin limit from g_spin_limit and
+// report a timeout through their result (kSegTimeout); the kernels set spin_err.
 // tests/test_kernarg_use.py checks the compiled IR.)
 __device__ __forceinline__ const EncodeArgs& enc_args_fresh() {
   const EncodeArgs* p = (const EncodeArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -373,11 +373,10 @@ __device__ __forceinline__ const EncodeArgs& enc_args_fresh() {
   return *p;
 }
 
-// The look-back's safety net, passed down from the kernel's own arguments.
-struct SpinCtl {
-  uint32_t limit;  // polls before a look-back gives up (the client then goes to the exact path)
-  uint32_t* err;   // OR'ed with 1 when one did
-};
+// Polls before a fast-kernel look-back gives up (the client then goes to the exact
+// path and the launch reports FC_OVERFLOW_STALL): a device global, so the
+// out-of-line look-backs need no argument for it (test knob FEDCODEC_SPIN_LIMIT).
+__device__ uint32_t g_spin_limit = 1u << 24;
 
 __device__ __forceinline__ uint32_t div_clients(const EncodeArgs& a, uint32_t n) {
   if (a.div_l == 0) return n;  // nclients == 1
@@ -490,7 +489,7 @@ __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgc
 // pre1/pre2 (optional): this lane's status of tile t-1-lane, loaded earlier.
 template <int SPAN = kTE>  // elements per status slot (tile, or super-tile)
 __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int lane,
-                                        bool& slow, SpinCtl sc, bool have_pre = false,
+                                        bool& slow, bool& timeout, uint32_t limit, bool have_pre = false,
                                         uint64_t pre1 = 0, uint64_t pre2 = 0) {
   Seg S = seg_identity();
   int64_t base = (int64_t)t - 1;
@@ -517,11 +516,11 @@ __device__ __forceinline__ Seg lookback(const uint64_t* status_c, int32_t t, int
       const uint64_t need = k >= 63 ? ~0ull : ((2ull << k) - 1);
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > sc.limit) {  // safety net only: tickets guarantee progress
+      if (++spins > limit) {  // safety net only: tickets guarantee progress
         // (a timed-out look-back's fold is not a prefix: `slow` makes the caller re-encode the
         // client -- k_encode_exact's callers through the overflow flag; the fold itself runs on,
         // which keeps this cold path from changing the encoders' register allocation)
-        if (lane == 0) atomicOr(sc.err, 1u);
+        timeout = true;
         slow = true;
         k = 0;
         w1 = kFlagPre;
@@ -566,10 +565,11 @@ __device__ unsigned long long g_stamps[16];
 // tail is its newest tile's tail whenever that tile's body has >= 32 bits;
 // otherwise the scalar lookback() does the whole fold (rare: a nearly empty
 // tile).  Out of line: it keeps its registers off the common path.
-constexpr uint32_t kSegSlow = 0xFFFFFFFFu;  // lookback_deep's "a slow tile" result (has_nz)
+constexpr uint32_t kSegSlow = 0xFFFFFFFFu;     // lookback_deep's "a slow tile" result (has_nz)
+constexpr uint32_t kSegTimeout = 0xFFFFFFFEu;  // ... "gave up polling" (slow too; the kernel reports it)
 template <int SPAN = kTE>
 __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, int lane,
-                                          uint64_t pre1, uint64_t pre2, SpinCtl sc) {
+                                          uint64_t pre1, uint64_t pre2) {
   // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
   // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
   Seg S = seg_identity();  // fold of the newer windows already walked
@@ -591,10 +591,9 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
       const uint64_t need = pre ? ~0ull << (63 - (int)__clzll(pre)) : ~0ull;
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > sc.limit) {  // (safety net) the client goes to the exact path
-        if (lane == 0) atomicOr(sc.err, 1u);
+      if (++spins > g_spin_limit) {  // (safety net) the client goes to the exact path
         Seg r = seg_identity();
-        r.has_nz = kSegSlow;
+        r.has_nz = kSegTimeout;
         return r;
       }
       if (!valid) {
@@ -644,8 +643,9 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
     const uint32_t csum = (uint32_t)wave_sum_i((int32_t)contrib);
     if (__builtin_amdgcn_readlane(l1, 63) < 32u) {  // short newest body: exact scalar fold
       bool slow = false;
-      Seg r2 = lookback<SPAN>(status_c, t, lane, slow, sc);
-      if (slow) r2.has_nz = kSegSlow;
+      bool to = false;
+      Seg r2 = lookback<SPAN>(status_c, t, lane, slow, to, g_spin_limit);
+      if (slow) r2.has_nz = to ? kSegTimeout : kSegSlow;
       return r2;
     }
     r.tail = __builtin_amdgcn_readlane(l2, 63);  // the newest body holds the last 32 bits
@@ -684,11 +684,11 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
 // scalar lookback() does the fold.  No prefix within 64 tiles: lookback_deep().
 template <int SPAN>
 __device__ __noinline__ Seg lookback_vec_wait(const uint64_t* status_c, int32_t t, int lane, uint64_t pre1,
-                                              uint64_t pre2, SpinCtl sc);
+                                              uint64_t pre2);
 template <bool WAIT, int SPAN>
 __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32_t t, int lane,
-                                                 bool& slow, uint64_t pre1,
-                                                 uint64_t pre2, SpinCtl sc) {
+                                                 bool& slow, bool& timeout, uint64_t pre1,
+                                                 uint64_t pre2) {
   // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
   // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
   const int32_t ti = t - 64 + lane;
@@ -708,9 +708,10 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     p = pre ? 63 - (int)__clzll(pre) : 0;
     const uint64_t need = ~0ull << p;
     if (pre == 0 || (val & need) != need) {
-      Seg r = lookback_vec_wait<SPAN>(status_c, t, lane, pre1, pre2, sc);
-      if (r.has_nz == kSegSlow) {
+      Seg r = lookback_vec_wait<SPAN>(status_c, t, lane, pre1, pre2);
+      if (r.has_nz >= kSegTimeout) {
         slow = true;
+        timeout = r.has_nz == kSegTimeout;
         r = seg_identity();
       }
       return r;
@@ -722,9 +723,10 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     const uint64_t val = __ballot(valid);
     if (pre == 0) {  // no prefix in the window: walk 64-tile windows
       FC_COUNT(10, 1);
-      Seg r = lookback_deep<SPAN>(status_c, t, lane, pre1, pre2, sc);
-      if (r.has_nz == kSegSlow) {
+      Seg r = lookback_deep<SPAN>(status_c, t, lane, pre1, pre2);
+      if (r.has_nz >= kSegTimeout) {
         slow = true;
+        timeout = r.has_nz == kSegTimeout;
         r = seg_identity();
       }
       return r;
@@ -734,8 +736,8 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     if ((val & need) == need) break;
     FC_COUNT(9, 1);
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > sc.limit) {  // (safety net) the client goes to the exact path
-      if (lane == 0) atomicOr(sc.err, 1u);
+    if (++spins > g_spin_limit) {  // (safety net) the client goes to the exact path
+      timeout = true;
       slow = true;
       return seg_identity();
     }
@@ -807,16 +809,16 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
 // The waiting variant, out of line (a re-poll, or no prefix in the window).
 template <int SPAN>
 __device__ __noinline__ Seg lookback_vec_wait(const uint64_t* status_c, int32_t t, int lane, uint64_t pre1,
-                                              uint64_t pre2, SpinCtl sc) {
-  bool slow = false;
-  Seg r = lookback_vec_impl<true, SPAN>(status_c, t, lane, slow, pre1, pre2, sc);
-  if (slow) r.has_nz = kSegSlow;
+                                              uint64_t pre2) {
+  bool slow = false, to = false;
+  Seg r = lookback_vec_impl<true, SPAN>(status_c, t, lane, slow, to, pre1, pre2);
+  if (slow) r.has_nz = to ? kSegTimeout : kSegSlow;
   return r;
 }
 template <int SPAN = kTE>
 __device__ __forceinline__ Seg lookback_vec(const uint64_t* status_c, int32_t t, int lane, bool& slow,
-                                            uint64_t pre1, uint64_t pre2, SpinCtl sc) {
-  return lookback_vec_impl<false, SPAN>(status_c, t, lane, slow, pre1, pre2, sc);
+                                            bool& timeout, uint64_t pre1, uint64_t pre2) {
+  return lookback_vec_impl<false, SPAN>(status_c, t, lane, slow, timeout, pre1, pre2);
 }
 
 // Runtime-indexed read of a small register array without scratch (select chain).
@@ -2064,7 +2066,9 @@ __global__ __launch_bounds__(kEncThreads, FC_ENC_WAVES) void k_encode(EncodeArgs
         excl.has_nz = 1;
         excl.first = excl.last = -1;
       } else {
-        excl = lookback_vec(a.status + 2 * (int64_t)pc * a.T, pt, lane, slow, pw1, pw2, SpinCtl{a.spin_limit, a.spin_err});
+        bool to = false;
+        excl = lookback_vec(a.status + 2 * (int64_t)pc * a.T, pt, lane, slow, to, pw1, pw2);
+        if (to && lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
         if (FC_ABL & 4096) {  // diagnostics: the look-back runs, its result is dropped
           asm volatile("" :: "s"((uint32_t)excl.body), "s"(excl.last), "s"(excl.tail));
           excl = seg_identity();
@@ -2565,8 +2569,9 @@ __global__ __launch_bounds__(kEncThreads * kEnc2Waves, FC_ENC_WAVES) void k_enco
           st_agent2(st, agg_word(fr, lr, body), kFlagAgg | agg_tail);
         }
         STAMP(5);
-        excl = lookback_vec<STE>(status_f + 2 * (int64_t)c * a.T, t2, lane, slow, pw1, pw2,
-                                 SpinCtl{a.spin_limit, a.spin_err});
+        bool to = false;
+        excl = lookback_vec<STE>(status_f + 2 * (int64_t)c * a.T, t2, lane, slow, to, pw1, pw2);
+        if (to && lane == 0) atomicOr(enc_args_fresh().spin_err, 1u);
         STAMP(6);
       }
     }
@@ -2737,7 +2742,9 @@ __global__ __launch_bounds__(kEncThreads) void k_encode_exact(EncodeArgs a) {
       bool slow = false;
       // (one global ticket counter: progress is unconditional here, so the test knob
       // FEDCODEC_SPIN_LIMIT does not apply; the limit stays a safety net)
-      excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, slow, SpinCtl{1u << 24, a.spin_err});
+      bool to = false;
+      excl = lookback(a.status + 2 * (int64_t)c * a.T, t, lane, slow, to, 1u << 24);
+      if (to && lane == 0) atomicOr(a.spin_err, 1u);
       // (only a timed-out look-back: every status here is the exact kernel's own) the
       // client's code is unusable; its overflow flag makes the checked caller re-encode it
       if (slow && lane == 0)
@@ -3381,8 +3388,11 @@ __device__ __forceinline__ void decode_segment(const uint8_t* base, int64_t cap,
       const int32_t rel_now = ((int32_t)(relb - my_addr)) >> 2;
       uint32_t rel_new = (uint32_t)(rel_now + (int32_t)d);
       // a segment's first nonzero after a run of >= 2^27 zeros: the index's previous
-      // nonzero is known modulo 2^28 only (FC_MAX_ELEMS), and so is the sum
-      if (rel_new >= span) rel_new &= kIdxLastMask;
+      // nonzero is known modulo 2^28 only (FC_MAX_ELEMS), and so is the sum.  Only the
+      // segment's first code (nothing consumed yet: its run starts at the index's
+      // nonzero) is reduced; a later code's run starts inside the tile, so one that
+      // leaves it is malformed (it used to be wrapped back in, unflagged)
+      if (rel_new >= span && cons == 0) rel_new &= kIdxLastMask;
       bad |= rel_new >= span ? 1u : 0u;
       relb = my_addr + 4u * min(rel_new, span - 1);
       acc_add_at<PLANE>(relb, v, ptile, hib, err);
@@ -5523,6 +5533,24 @@ __global__ void k_quarter_index(const uint64_t* __restrict__ idx, uint64_t* __re
   }
 }
 
+// The fast encoders' look-back spin limit (g_spin_limit): 2^24 polls, or the test knob
+// FEDCODEC_SPIN_LIMIT; written to the device only when it changes (per device).
+int set_spin_limit() {
+  static std::mutex mu;
+  static std::map<int, uint32_t> cur;
+  uint32_t want = 1u << 24;
+  if (const char* e = getenv("FEDCODEC_SPIN_LIMIT")) want = (uint32_t)std::max(1L, atol(e));  // test knob
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(-10, "hipGetDevice");
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cur.find(dev);
+  if (it != cur.end() && it->second == want) return 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_spin_limit), &want, sizeof(want)) != hipSuccess)
+    return fail(-10, "g_spin_limit");
+  cur[dev] = want;
+  return 0;
+}
+
 int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step, const float* norms,
                   const float* prescale, const int64_t* seeds, int mode, bool int_in, uint8_t* stream_buf,
                   const int64_t* stream_off, const int64_t* stream_cap, uint64_t* idx,
@@ -5571,8 +5599,7 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   a.slow_count = a.counter + kShardStride * (kTicketShards + 2);
   a.started = a.counter + kShardStride * (kTicketShards + 3);
   a.slow_flag = (int32_t*)(a.counter + kHdrWords);
-  a.spin_limit = 1u << 24;
-  if (const char* e = getenv("FEDCODEC_SPIN_LIMIT")) a.spin_limit = (uint32_t)std::max(1L, atol(e));  // test knob
+  if (const int rc = set_spin_limit()) return rc;
   a.by_block = 0;
   if (const char* e = getenv("FEDCODEC_TICKET_BLOCKIDX")) a.by_block = atoi(e) != 0;  // regression-test knob
   a.slow_list = a.slow_flag + nclients;

@@ -251,3 +251,61 @@ def test_config5_onebit_at_25M(gpu):
   np.testing.assert_allclose(np.mean(dist.cpu().numpy()) / P, meas["avg_distortion"], rtol=1e-5)
   del rows
   _release()
+
+
+def test_config5_onebit_round_full_size(gpu):
+  """Config 5's whole codec round on one GPU: 1024 clients x 25 M, one-bit SGD
+  (one_bit_sgd.py:45-112) through distributed.onebit_round (the round the 8-GPU run
+  shards).  Oracle checks the size allows:
+    * every client's mask bits at 20,000 sampled positions (x >= threshold), and
+      four clients' whole masks;
+    * 16 clients' means and distortions against numpy float64 over their full rows
+      (rtol 1e-6 / 1e-5; TF's float32 reduction order is unspecified);
+    * the round's decoded sum at the sampled positions: the client-order float32
+      sum of each client's mean selected by its bit (one_bit_sgd.py:87-112), bit
+      for bit given the means;
+    * measurements: avg_bitrate = (P + 64) / P, avg_distortion."""
+  from federated_amd import distributed  # pylint: disable=g-import-not-at-top
+  C, P, thr = 1024, 25_000_000, 0.0
+  g = torch.Generator(device=gpu)
+  rows = []
+  for c in range(C):
+    g.manual_seed(5000 + c)
+    rows.append(torch.randn(P, generator=g, device=gpu, dtype=torch.float32) * (0.5 + (c % 5) * 0.25) + 0.01 * (c % 3))
+  rnd = distributed.onebit_round(rows, thr, multi=False)
+  masks, means, dist = codec.onebit_encode(rows, thr)  # the round's own encode, for the checks
+  res = rnd.result.cpu().numpy()
+  nw = (P + 31) // 32
+  means_h = means.cpu().numpy().reshape(C, 2)
+  dist_h = dist.cpu().numpy()
+  # masks at sampled positions, every client
+  idx = np.sort(np.random.default_rng(55).choice(P, 20_000, replace=False))
+  it = torch.from_numpy(idx).to(gpu)
+  vals = torch.stack([r[it] for r in rows]).cpu().numpy()
+  words = masks.view(C, nw)[:, torch.from_numpy(idx // 32).to(gpu)].cpu().numpy().view(np.uint32)
+  bits = ((words >> (idx % 32).astype(np.uint32)) & 1).astype(bool)
+  np.testing.assert_array_equal(bits, oq.ftz(vals) >= F32(thr))
+  # whole masks and means / distortions of sampled clients against float64 numpy
+  for c in (0, 1, 511, 1023):
+    x = oq.ftz(rows[c].cpu().numpy())
+    b = np.pad((x >= thr).astype(np.uint8), (0, nw * 32 - P)).reshape(nw, 32)
+    np.testing.assert_array_equal(masks.view(C, nw)[c].cpu().numpy().view(np.uint32),
+                                  np.packbits(b, axis=1, bitorder="little").view("<u4").reshape(-1))
+  for c in range(0, C, C // 16):
+    x = oq.ftz(rows[c].cpu().numpy())
+    ab = x >= thr
+    xd = x.astype(np.float64)
+    mb, ma = xd[~ab].sum() / max((~ab).sum(), 1), xd[ab].sum() / max(ab.sum(), 1)
+    np.testing.assert_allclose(means_h[c], [mb, ma], rtol=1e-6)
+    dec = np.where(ab, means_h[c, 1], means_h[c, 0]).astype(np.float32)
+    np.testing.assert_allclose(dist_h[c], ((x - dec).astype(np.float64) ** 2).sum(), rtol=1e-5)
+  # the decoded client-order float32 sum at the sampled positions
+  acc = np.zeros(idx.size, np.float32)
+  for c in range(C):
+    acc = (acc + np.where(bits[c], means_h[c, 1], means_h[c, 0]).astype(np.float32)).astype(np.float32)
+  np.testing.assert_array_equal(res[idx].view(np.uint32), acc.view(np.uint32))
+  m = rnd.measurements
+  assert m["avg_bitrate"] == F32((F32(P) + F32(64.0)) / F32(P))
+  np.testing.assert_allclose(m["avg_distortion"], np.mean(dist_h / P), rtol=1e-5)
+  del rows, masks, means, dist, rnd
+  _release()

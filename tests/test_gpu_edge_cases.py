@@ -148,3 +148,47 @@ def test_capacity_hint_sizes_the_next_round(gpu):
   assert not len(codec.check_overflow(b2))
   assert hint.caps(P, C)[0] < codec.worst_case_capacity(P)
   np.testing.assert_array_equal(b2.bits() > 9 * P, np.ones(C, bool))
+
+
+def _gamma_bits(n):
+  """Elias gamma of n >= 1 as a bit string (TFC run-length gamma, elias_gamma_encode.py:30-45)."""
+  b = bin(int(n))[2:]
+  return "0" * (len(b) - 1) + b
+
+
+def test_oversized_run_inside_a_segment_is_flagged(gpu):
+  """the decoder reduces a run modulo 2^28 only for a segment's FIRST code
+  (whose run starts at the index's previous nonzero, kept modulo 2^28).  A later code
+  whose run leaves the tile is malformed and must set err -- before the fix, a run of
+  2^28 + 5 from element 0 wrapped back to element 5 and was summed, unflagged.  The
+  stream is decoded through an encoder-style index (not rebuilt from the bytes)."""
+  P = 1024
+  bits = _gamma_bits(1) + "1" + _gamma_bits(1)                # element 0: +1
+  bits += _gamma_bits((1 << 28) + 5) + "1" + _gamma_bits(1)  # run 2^28 + 5 (57 bits): out of the tile
+  nbits = len(bits)
+  padded = bits + "0" * (-nbits % 8)
+  code = bytes(int(padded[i:i + 8], 2) for i in range(0, len(padded), 8))
+  batch = codec.EncodedBatch(P, 1, [256], gpu)
+  buf = np.zeros(batch.stream.numel(), np.uint8)
+  buf[:len(code)] = np.frombuffer(code, np.uint8)
+  batch.stream.copy_(torch.from_numpy(buf).to(gpu))
+  # encoder index of one tile: starts at bit 0 with no earlier nonzero; the tile's
+  # codes end at nbits (no trailing code), its last nonzero claimed at element 5
+  batch.idx.copy_(torch.tensor([0, nbits | (6 << 36)], dtype=torch.int64, device=gpu))
+  batch.total_bits.fill_(nbits)
+  s, _, err = codec.decode_accumulate(batch)
+  assert int(err.item()) != 0
+  # the well-formed prefix alone (element 0 only) decodes cleanly
+  ok_bits = _gamma_bits(1) + "1" + _gamma_bits(1) + _gamma_bits(P)
+  padded = ok_bits + "0" * (-len(ok_bits) % 8)
+  code = bytes(int(padded[i:i + 8], 2) for i in range(0, len(padded), 8))
+  buf[:] = 0
+  buf[:len(code)] = np.frombuffer(code, np.uint8)
+  batch.stream.copy_(torch.from_numpy(buf).to(gpu))
+  head = len(ok_bits) - len(_gamma_bits(P))
+  batch.idx.copy_(torch.tensor([0, head | (1 << 36)], dtype=torch.int64, device=gpu))
+  s, _, err = codec.decode_accumulate(batch)
+  assert int(err.item()) == 0
+  want = np.zeros(P, np.int32)
+  want[0] = 1
+  np.testing.assert_array_equal(s.cpu().numpy(), want)
