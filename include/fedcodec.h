@@ -2,10 +2,14 @@
  *
  * C ABI of libfedcodec.so (federated_amd/csrc/fedcodec.hip, gfx950 only).
  * Plain pointers and sizes; every device pointer is caller-owned HBM; every
- * entry is asynchronous on the given hipStream_t (passed as void*) and never
- * synchronises, allocates or frees.  Return 0 on success, a negative code on a
- * rejected argument (message from fc_last_error(), thread-local); no C++
- * exception crosses the ABI.
+ * entry is asynchronous on the given hipStream_t (passed as void*).  Two
+ * library-owned exceptions, both outside steady state: fc_client_norms(_scaled),
+ * fc_onebit_encode and fc_drive_encode keep a small grow-only partials buffer per
+ * (device, stream), allocated on the first call of a size (a call under graph
+ * capture that would have to grow it fails with -1: warm it uncaptured); the
+ * encoders write their look-back spin limit (a device global) on the first call
+ * per device.  Return 0 on success, a negative code on a rejected argument
+ * (message from fc_last_error(), thread-local); no C++ exception crosses the ABI.
  *
  * Reference interfaces replaced (file:line under google-research/federated):
  *   fc_quantize            quantize_utils.uniform_quantize / stochastic_quantize /

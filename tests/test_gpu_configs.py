@@ -71,11 +71,17 @@ def _hip_quantize_sum(rows, step, seeds, mode):
 
 
 def _check_codes(batch, xs_host, clients, step, seeds, mode):
-  for c in clients:
+  """Byte-exact codes of `clients` against the oracle (quantiser + C coder on a thread pool)."""
+  bits = batch.bits()
+
+  def one(c):
     q = ORACLE_Q[mode](xs_host[c], F32(step), tuple(seeds[c]))
     code, nbits = ocodec.run_length_gamma_encode(q)
-    assert int(batch.bits()[c]) == nbits, c
-    assert batch.client_code(c) == code, c
+    return c, nbits, code
+  with ThreadPoolExecutor(WORKERS) as ex:
+    for c, nbits, code in ex.map(one, clients):
+      assert int(bits[c]) == nbits, c
+      assert batch.client_code(c) == code, c
 
 
 def _round(rows, step, seeds, mode):
@@ -126,7 +132,9 @@ def test_headline_shape_round(gpu, C, mode):
     rows.append(torch.randn(P, generator=g, device=gpu, dtype=torch.float32))
   seeds = np.array([[1000 + c, 1000 + c] for c in range(C)], np.int64)
   batch, s, out = _round(rows, step, seeds, mode)
-  picks = (0, C // 2, C - 1)
+  # sixteen clients' codes byte for byte against the oracle, spread over the batch (the
+  # first and last clients, the 32nd-34th, every eighth of the batch)
+  picks = sorted(set([0, 1, 2, 31, 32, 33] + [C * k // 8 for k in range(1, 8)] + [C - 3, C - 2, C - 1]))
   _check_codes(batch, {c: rows[c].cpu().numpy() for c in picks}, picks, step, seeds, mode)
   want = _hip_quantize_sum(rows, step, seeds, mode)
   assert torch.equal(s, want)

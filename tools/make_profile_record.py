@@ -110,6 +110,13 @@ def main():
                                           "fetch_raw_bytes": mean(v["FETCH_SIZE"]) * 1024.0,
                                           "write_raw_bytes": mean(v["WRITE_SIZE"]) * 1024.0}
                                       for n, v in inst.items() if n not in timed}}
+    if "k_decode" in out:
+      out["k_decode"]["fetch_note"] = (
+          "FETCH_SIZE counts L2-miss bytes (served by the MALL or HBM; the TCC counters cannot split them). "
+          "The decoder's lanes stream their own segments in 16-byte loads and its L2 re-fetches lines "
+          "between reads: a raw FETCH above the code bytes is that re-fetch (64-byte chunks per lane bring "
+          "it to 1.07x, profiles/r04), recorded with multiplier 1 -- no calibration factor is applied "
+          "(round 3's 2.54x calibration kernel has the same access pattern, DESIGN.md section 5)")
     out["workload"] = w
     out["command"] = "tools/profile_workloads.sh <out> %s (bench.py --workload %s)" % (w, w)
     with open(os.path.join(dst, "traffic_%s.json" % w), "w") as fh:
