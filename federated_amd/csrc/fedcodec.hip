@@ -1450,8 +1450,13 @@ struct alignas(64) ClientParam {
   int64_t gofs;              // Philox group of x[0]: elem_off[c] / 4 (segments), else 0
 };
 
-__global__ void k_client_params(EncodeArgs a, ClientParam* cp, int need_key) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// Also zeroes the launch's look-back statuses, ticket counters and slow-client flags
+// (nzero16 16-byte words from `zero`): one prologue launch instead of a memset plus
+// this kernel.
+__global__ void k_client_params(EncodeArgs a, ClientParam* cp, int need_key, uint4* zero, int64_t nzero16) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = i0; i < nzero16; i += (int64_t)gridDim.x * blockDim.x) zero[i] = make_uint4(0, 0, 0, 0);
+  const int c = (int)i0;
   if (c >= a.nclients) return;
   ClientParam p;
   p.step = a.norms ? a.norms[c] * a.step : a.step;
@@ -5571,7 +5576,6 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
   hipStream_t s = (hipStream_t)stream;
   const int64_t T = tiles_for(P);
   const int64_t sb = enc_status_bytes(nclients, P);
-  if (hipMemsetAsync(workspace, 0, enc_zeroed_bytes(nclients, P), s) != hipSuccess) return fail(-10, "memset status");
   EncodeArgs a;
   a.elem_off = elem_off;
   a.idxq = idxq;
@@ -5697,8 +5701,14 @@ int encode_common(const void* const* xs, int32_t nclients, int64_t P, float step
     if (const char* w = getenv("FEDCODEC_LB_WIN")) win = atoi(w);  // test knob
     a.lb_lane0 = 64 - std::max(1, std::min(64, win));
   }
-  hipLaunchKernelGGL(k_client_params, dim3((nclients + 255) / 256), dim3(256), 0, s, a,
-                     (ClientParam*)a.cparams, (int)(!int_in && mode != FC_UNIFORM));
+  {  // prologue: the zeroed workspace prefix (statuses, counters, slow flags; rounded up to
+     // 16 bytes, below the client parameters) and the client parameters
+    const int64_t nzero16 = (enc_zeroed_bytes(nclients, P) + 15) / 16;
+    const int64_t blocks = std::max<int64_t>((nclients + 255) / 256,
+                                             std::min<int64_t>((nzero16 + 255) / 256, (int64_t)ncu * 8));
+    hipLaunchKernelGGL(k_client_params, dim3((unsigned)blocks), dim3(256), 0, s, a, (ClientParam*)a.cparams,
+                       (int)(!int_in && mode != FC_UNIFORM), (uint4*)workspace, nzero16);
+  }
   if (hipGetLastError() != hipSuccess) return fail(-10, "k_client_params launch");
   hipLaunchKernelGGL(kern, dim3((grid + wpg - 1) / wpg), dim3(kEncThreads * wpg), 0, s, a);
   if (const int rc_ = check_launch("k_encode")) return rc_;
