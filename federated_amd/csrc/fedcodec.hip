@@ -57,25 +57,37 @@ constexpr uint32_t kNoPos = 0x3FFF; // "no nonzero" in a 14-bit (super-)tile-rel
 // (MI355X_MICROARCH.md "dequeue"), so tickets come from kTicketShards counters,
 // one 64-B line each; stream k hands out tickets k, k + K, k + 2K, ... in order.
 constexpr int kTicketShards = 32;
-// A wave draws from stream (r mod K), r = its START ORDER (a per-launch counter every
-// wave increments once when it begins), not from its blockIdx.  Progress: the
+constexpr int kShardStride = 16;  // uint32 words between counters (64 B)
+// A wave's stream comes from its START ORDER, not from its blockIdx.  Progress: the
 // smallest ticket m nobody has taken belongs to stream s; every wave of stream s
 // holds only tickets below m, whose predecessors are all taken, so (by induction on
 // m) they finish and one of them takes m -- provided stream s has a wave that has
-// started.  With start-order streams the first K waves that start cover all K
-// streams, and a started wave stays resident until its stream is exhausted, so any
-// K co-resident waves suffice (two wavefronts' worth of CUs).  With blockIdx streams
-// (round 5) a stream whose workgroups were not resident -- another kernel holding
-// their CUs, e.g. a second process's persistent encoder on the same GPU -- left
-// every resident wave spinning in the look-back until the spin limit
-// (DESIGN.md §2 "Ticket streams and progress").  FEDCODEC_TICKET_BLOCKIDX=1 restores
-// that mapping for the regression test only.
+// started, and a started wave stays resident until its stream is exhausted.
+// With blockIdx streams (round 5) a stream whose workgroups were not resident --
+// another kernel holding their CUs, e.g. a second process's persistent encoder on
+// the same GPU -- left every resident wave spinning in the look-back until the spin
+// limit (DESIGN.md §2 "Ticket streams and progress").
+// Start order is counted on kStartHeads heads (64-B lines), head h = a hash of the
+// wave's index: its n-th started wave takes stream (h + n) mod K.  One head per
+// launch (any K started waves cover all K streams) or one per XCD cost 60-70 us per
+// encoder launch in contention at configs 3 and 4 (one dequeue word saturates near
+// 90/us, MI355X_MICROARCH.md "dequeue"; profiles/r06/diag_start_heads.txt); 32 heads
+// cost nothing measurable.  A head with K started waves covers every stream, so any
+// kStartHeads * K started waves suffice (pigeonhole: a quarter of an idle chip's
+// grid), and fewer usually do (waves of one XCD land on heads spread over all
+// offsets).  Below that the spin limit remains the safety net: the client goes to
+// the exact path and the launch reports FC_OVERFLOW_STALL.
+// FEDCODEC_TICKET_BLOCKIDX=1 restores round 5's mapping for the regression demo only.
+constexpr int kStartHeads = 32;
 __device__ __forceinline__ uint32_t ticket_stream(uint32_t* started, uint32_t b, uint32_t w, uint32_t wpg,
                                                   uint32_t nshards, uint32_t by_block, int lane) {
+  const uint32_t g = b * wpg + w;
+  if (by_block) return g % nshards;
+  const uint32_t h = (g + (g >> 5)) % (uint32_t)kStartHeads;
   uint32_t r = 0;
-  if (lane == 0) r = atomicAdd(started, 1u);
+  if (lane == 0) r = atomicAdd(started + kShardStride * h, 1u);
   r = __builtin_amdgcn_readfirstlane(r);
-  return (by_block ? b * wpg + w : r) % nshards;
+  return (r + h) % nshards;
 }
 #ifndef FC_STORE_ALIGN
 #define FC_STORE_ALIGN 1
@@ -89,7 +101,6 @@ constexpr bool kStoreAlign = FC_STORE_ALIGN;
 #define FC_LOOKBACK_WIN 0  // 0: chosen per launch from the tiles in flight per client
 #endif
 constexpr int kLookbackWin = FC_LOOKBACK_WIN;  // statuses prefetched for the vector look-back
-constexpr int kShardStride = 16;  // uint32 words between counters (64 B)
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 and TF's stateless seed scramble (see oracle/philox.py).
@@ -376,7 +387,11 @@ __device__ __forceinline__ const EncodeArgs& enc_args_fresh() {
 // Polls before a fast-kernel look-back gives up (the client then goes to the exact
 // path and the launch reports FC_OVERFLOW_STALL): a device global, so the
 // out-of-line look-backs need no argument for it (test knob FEDCODEC_SPIN_LIMIT).
-__device__ uint32_t g_spin_limit = 1u << 24;
+// In the constant address space, so it is a scalar load, and read once per call
+// before the poll loop: as a plain global it compiled to a vector load plus a
+// `vmcnt(0)` in every poll -- waiting on the wave's pending code stores and staging
+// loads each time (+8-10 % encode time at configs 2-4, profiles/r06/diag_spin_limit_ab.txt).
+__constant__ uint32_t g_spin_limit = 1u << 24;
 
 __device__ __forceinline__ uint32_t div_clients(const EncodeArgs& a, uint32_t n) {
   if (a.div_l == 0) return n;  // nclients == 1
@@ -573,6 +588,7 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
   // Everything on 32-bit halves: h = granule bits [63:32] (flag in [31:30]),
   // l = bits [31:0].  ti < 0: the virtual root prefix (last + 1 = 0, body 0).
   Seg S = seg_identity();  // fold of the newer windows already walked
+  const uint32_t lim = g_spin_limit;
   int32_t wbase = t - 64;
   uint32_t h1 = (uint32_t)(pre1 >> 32), l1 = (uint32_t)pre1, h2 = (uint32_t)(pre2 >> 32), l2 = (uint32_t)pre2;
   for (;;) {
@@ -591,7 +607,7 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
       const uint64_t need = pre ? ~0ull << (63 - (int)__clzll(pre)) : ~0ull;
       if ((val & need) == need) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > g_spin_limit) {  // (safety net) the client goes to the exact path
+      if (++spins > lim) {  // (safety net) the client goes to the exact path
         Seg r = seg_identity();
         r.has_nz = kSegTimeout;
         return r;
@@ -644,7 +660,7 @@ __device__ __noinline__ Seg lookback_deep(const uint64_t* status_c, int32_t t, i
     if (__builtin_amdgcn_readlane(l1, 63) < 32u) {  // short newest body: exact scalar fold
       bool slow = false;
       bool to = false;
-      Seg r2 = lookback<SPAN>(status_c, t, lane, slow, to, g_spin_limit);
+      Seg r2 = lookback<SPAN>(status_c, t, lane, slow, to, lim);
       if (slow) r2.has_nz = to ? kSegTimeout : kSegSlow;
       return r2;
     }
@@ -718,6 +734,7 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     }
   }
   uint32_t spins = 0;
+  const uint32_t lim = WAIT ? g_spin_limit : 0u;
   for (; WAIT;) {
     const uint64_t pre = __ballot(valid && h1 >= 0x80000000u);  // inclusive prefix (or slow)
     const uint64_t val = __ballot(valid);
@@ -736,7 +753,7 @@ __device__ __forceinline__ Seg lookback_vec_impl(const uint64_t* status_c, int32
     if ((val & need) == need) break;
     FC_COUNT(9, 1);
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > g_spin_limit) {  // (safety net) the client goes to the exact path
+    if (++spins > lim) {  // (safety net) the client goes to the exact path
       timeout = true;
       slow = true;
       return seg_identity();
@@ -5498,9 +5515,9 @@ int launch_mask_encode(const float* const* xs, int32_t nclients, int64_t P, floa
 
 
 // Workspace: [status n*T*16][header: ticket shards, spin_err, counter2,
-// slow_count, started][slow_flag n*4] (all zeroed per launch) [slow_list n*4]
+// slow_count, start heads][slow_flag n*4] (all zeroed per launch) [slow_list n*4]
 // [ClientParam n*64].
-constexpr int kHdrWords = kShardStride * (kTicketShards + 4);
+constexpr int kHdrWords = kShardStride * (kTicketShards + 3 + kStartHeads);
 int64_t enc_status_bytes(int32_t n, int64_t P) { return (int64_t)n * tiles_for(P) * 16; }
 int64_t enc_zeroed_bytes(int32_t n, int64_t P) {
   return enc_status_bytes(n, P) + 4 * kHdrWords + 4 * (int64_t)n;
