@@ -307,8 +307,8 @@ __device__ __forceinline__ void st_agent2(uint64_t* p, uint64_t g0, uint64_t g1)
   const u32x4 v = {(uint32_t)g0, (uint32_t)(g0 >> 32), (uint32_t)g1, (uint32_t)(g1 >> 32)};
   // `s_nop 1` inside the statement: a store of more than 8 bytes reads its data
   // VGPRs after issue, and the compiler does not see the store to pad the VALU
-  // write that may follow (gfx9 hazard; without it a status could go out with
-  // half-overwritten words -- the round-5 / round-6 illegal-address faults, DESIGN
+  // write that may follow (a gfx9 hazard: a status could go out with half-overwritten
+  // words; no instance was found in the listings, but nothing prevented one -- DESIGN
   // §2 "Ticket streams and progress")
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
