@@ -3648,8 +3648,11 @@ constexpr int64_t kIdxFail = -1;  // "the parse failed" (a guessed start, or pas
 // guessed one is a true code start, and its last nonzero follows from the chunk's
 // true runs, so k_idx_emit parses from the checkpoint before each unit boundary
 // instead of the whole chunk.
-// per chunk: nck = min(15, chunk / 256 - 1) checkpoints, chunk / (nck + 1) bits apart
-inline int32_t idx_nck(int32_t chunk) { return std::min(15, chunk / 256 - 1); }
+// per chunk: nck = min(FC_IDX_NCK_MAX, chunk / 256 - 1) checkpoints, chunk / (nck + 1) bits apart
+#ifndef FC_IDX_NCK_MAX
+#define FC_IDX_NCK_MAX 31  // checkpoints per chunk at most (15: the headline's rebuild +0.5 ms, profiles/r06/diag_idx_emit.txt)
+#endif
+inline int32_t idx_nck(int32_t chunk) { return std::min(FC_IDX_NCK_MAX, chunk / 256 - 1); }
 #ifndef FC_IDX_ASYNC
 #define FC_IDX_ASYNC 0
 #endif
