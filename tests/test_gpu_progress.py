@@ -4,8 +4,9 @@ Round 5's one GPU fault (`profiles/r05/gputest_fault_r5zz.txt`) came from two
 processes on one GPU running persistent encoders side by side: with ticket streams
 tied to blockIdx, a stream whose workgroups were not resident left every resident
 wave spinning in the look-back until its spin limit.  The encoder now draws its
-ticket stream from its START ORDER (fedcodec.hip `ticket_stream`), so any 32
-started waves cover every stream.
+ticket stream from its START ORDER (fedcodec.hip `ticket_stream`: counted on 32
+heads, a head's n-th started wave takes stream h + n), so the waves that did start
+cover every stream.
 
 Here one process does what the second process did: `fc_diag_occupy` holds every CU
 of one XCD (160 KiB of LDS each) for longer than the spin limit while the encoder
