@@ -1,6 +1,6 @@
 """Diagnostic: HIP-event time of k_encode / k_decode for one library build.
 
-FEDCODEC_LIB=federated_amd/libfedcodec_<variant>.so C=1024 P=25000000 MODE=1 STEP=0.5 \
+FEDCODEC_LIB=federated_amd/libfedcodec_<variant>.so C=1024 P=25000000 MODE=1 STEP=0.5 [CLIP=3.7] \
     python tools/enc_bench.py
 Prints one line: variant, encode ms (median of REPS), decode ms, bits/element.
 """
@@ -39,6 +39,10 @@ else:
     r = big[off[c]:off[c] + P]
     r.copy_(torch.randn(P, generator=g, device=dev))
     rows.append(r)
+CLIP = float(os.environ.get("CLIP", 0))  # > 0: rows clamped to [-CLIP, CLIP] (e.g. every |q| <= 7)
+if CLIP > 0:
+  for r in rows:
+    r.clamp_(-CLIP, CLIP)
 print("row bases mod 2 MiB:", sorted(set(r.data_ptr() % (1 << 21) for r in rows))[:8], flush=True)
 ptrs = torch.tensor([r.data_ptr() for r in rows], dtype=torch.int64, device=dev)
 seeds = torch.tensor([[c, c] for c in range(C)], dtype=torch.int64, device=dev)
