@@ -40,7 +40,7 @@ def test_host_only_entry_points():
 
 def test_index_workspace_follows_the_chunk_choice():
   """fc_build_index's chunk lanes: the largest of 8192 / 4096 / 2048 bits giving about
-  600 K lanes, min(15, chunk / 256 - 1) checkpoints each; the workspace holds five int64
+  600 K lanes, min(31, chunk / 256 - 1) checkpoints each; the workspace holds five int64
   and the checkpoints per lane, plus an int32 per client."""
   lib = _lib.load()
 
@@ -49,7 +49,7 @@ def test_index_workspace_follows_the_chunk_choice():
     while cb > 2048 and n * -(-8 * max_bytes // cb) < 600_000:
       cb //= 2
     lanes = n * max(1, -(-8 * max_bytes // cb))
-    return (5 + min(15, cb // 256 - 1)) * 8 * lanes + ((4 * n + 255) & ~255)
+    return (5 + min(31, cb // 256 - 1)) * 8 * lanes + ((4 * n + 255) & ~255)
 
   for n, mb in [(1024, 12_300_000), (256, 1_400_000), (128, 1_360_000), (2, 100), (1, 0), (300, 15_872)]:
     assert lib.fc_index_workspace_bytes(n, mb) == want(n, mb), (n, mb)
